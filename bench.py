@@ -1,0 +1,214 @@
+#!/usr/bin/env python3
+"""bench.py -- decisions/s of the MI355X rate-limit decision engine.
+
+Workload (BASELINE.json configs[1], the metric's single-GPU config):
+  Token Bucket "100/min burst 20" == {Limit 20, Window 12 s}; 1M keys Zipf
+  s=1.1 (rank->id seeded permutation, seed 2); arrivals exp(mean 1 us) from
+  t0 = 1.76e18 ns (seed 3); n = 1; batches of 1M requests.
+A step = one batch through the full engine path (probe/insert into the HBM
+table, radix sort by slot, segment discovery, per-key replay with exact Redis
+Lua "%.14g" semantics), inputs already resident in HBM, results written to HBM.
+
+Multi-GPU (torchrun, one rank per GPU): the key space shards by owner; each
+rank decides its own shard's requests (no data-path collective: the shards
+are independent), so per-GPU work is fixed -> "scaling": "weak".
+
+Prints one JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "distributed-rate-limiter_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STATE_BYTES = {1: 24, 2: 48, 3: 32}  # S_TB, S_SW, S_FW
+
+
+def make_workload(name, batch, rank):
+    import traces
+    if name == "tb_zipf":
+        return traces.TokenBucketZipf(batch=batch, seed=3 + 1000 * rank)
+    if name == "fw_uniform":
+        return traces.FixedWindowUniform(batch=batch, seed=1 + 1000 * rank)
+    if name == "sw_bursty":
+        return traces.SlidingWindowBursty(batch=batch, seed=4 + 1000 * rank)
+    if name == "mixed":
+        return traces.MixedTenants(batch=batch, seed=5 + 1000 * rank)
+    raise SystemExit(f"unknown workload {name}")
+
+
+WORKLOAD_DESC = {
+    "tb_zipf": "configs[1]: Token Bucket 100/min burst 20 (Limit 20, Window 12s), 1M keys Zipf s=1.1, batch 1M",
+    "fw_uniform": "configs[0]: Fixed Window 100/min, 10k uniform keys",
+    "sw_bursty": "configs[2]: Sliding Window 100/min, 100M keys, uniform + bursty",
+    "mixed": "configs[3]: mixed TB/SW/FW by key mod 3, 1B keys uniform",
+}
+
+
+def cpu_baseline(workload, batch, sample):
+    """The CPU restatement (oracle/, C, one core) timed on a bounded sample of
+    the same workload on this host (cpu_baseline leg: test infrastructure)."""
+    import oracle
+    gen = make_workload(workload, min(batch, sample), 0)
+    sim = oracle.OracleSim(oracle.REDIS7)
+    for a, L, W in gen.configs:
+        sim.add_config(a, L, W)
+    done, t = 0, 0.0
+    while done < sample:
+        key, ts, n, cfg = gen.next_batch()
+        t0 = time.perf_counter()
+        sim.decide(key, ts, n, cfg)
+        t += time.perf_counter() - t0
+        done += key.size
+    return {"value": done / t, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "sample": f"{done} requests of the same workload through oracle/rl_oracle.c "
+                      f"(C restatement of Go+Redis Lua, glibc %.14g/strtod), single thread"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--workload", default="tb_zipf", choices=sorted(WORKLOAD_DESC))
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import rl_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")  # RCCL over xGMI: barrier + max-over-ranks only
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    gen = make_workload(args.workload, args.batch, rank)
+    nb = args.warmup + args.steps
+    host = [gen.next_batch() for _ in range(nb)]
+    # this rank's shard of the key space: ids tagged with the owner rank
+    tag = np.uint64(rank) << np.uint64(48)
+    uniq = np.unique(host[-1][0]).size
+    dev_batches = []
+    for key, ts, n, cfg in host:
+        dev_batches.append((
+            torch.from_numpy((key | tag).view(np.int64)).to(dev),
+            torch.from_numpy(ts).to(dev),
+            torch.from_numpy(n).to(dev),
+            torch.from_numpy(cfg.view(np.int32)).to(dev),
+        ))
+    del host
+
+    algs = {a for a, _, _ in gen.configs}
+    need_tb = 1 in algs
+    keyspace = {"tb_zipf": 1 << 21, "fw_uniform": 1 << 15, "sw_bursty": 1 << 27, "mixed": 1 << 26}[args.workload]
+    eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7,
+                        tb_capacity=keyspace if need_tb else 1024,
+                        win_capacity=keyspace if algs - {1} else 1024,
+                        max_batch=args.batch, device=local_rank)
+    for a, L, W in gen.configs:
+        eng.register(a, L, W)
+    m = args.batch
+    out_dec = torch.empty(m, dtype=torch.uint8, device=dev)
+    out_rem = torch.empty(m, dtype=torch.int64, device=dev)
+    out_retry = torch.empty(m, dtype=torch.int64, device=dev)
+    out_reset = torch.empty(m, dtype=torch.int64, device=dev)
+    out_tok = torch.empty(m, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(b):
+        k, t, n, c = dev_batches[b]
+        eng.decide_device(m, k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
+                          out_dec.data_ptr(), out_rem.data_ptr(), out_retry.data_ptr(), out_reset.data_ptr(),
+                          out_tok.data_ptr(), stream)
+
+    for b in range(args.warmup):
+        step(b)
+    torch.cuda.synchronize()
+    rc = eng.sync()
+    if rc != 0:
+        raise SystemExit(f"engine error during warmup: {rc} {eng.last_error()}")
+    eng.set_timing(True)
+    eng.stage_times()  # clear
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(args.warmup, nb):
+        step(b)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    rc = eng.sync()
+    if rc != 0:
+        raise SystemExit(f"engine error during timed region: {rc} {eng.last_error()}")
+    stage_ms, nbat = eng.stage_times()
+    st = eng.stats()
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    decisions = args.steps * m * world
+    value = decisions / elapsed
+    # per-launch device time of each kernel (HIP events on the launch stream)
+    per_launch_ms = {
+        "probe": stage_ms[0] / nbat,
+        "sort_pass": stage_ms[1] / nbat / st.sort_passes,
+        "segments": stage_ms[2] / nbat,
+        "replay": stage_ms[3] / nbat,
+    }
+    dom = max(per_launch_ms, key=per_launch_ms.get)
+    s_alg = max(STATE_BYTES[a] for a in algs)
+    bytes_per_dec = 24 + 32 + 2 * s_alg * (uniq / m)
+    achieved = bytes_per_dec * m / (per_launch_ms[dom] / 1e3) / 1e9
+    out = {
+        "metric": "decisions/sec",
+        "value": value,
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
+        "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
+                   "profile": "redis7 (Lua %.14g state round trip)", "parallelism": f"key-shard x{world}"},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_decision": bytes_per_dec},
+        "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
+                                                    (stage_ms / nbat).tolist())},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.workload, m, args.cpu_sample)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

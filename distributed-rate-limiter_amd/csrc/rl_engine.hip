@@ -1,0 +1,529 @@
+// rl_engine.hip -- MI355X batched rate-limit decision engine: kernels + C-ABI.
+//
+// One batch = one launch sequence on the engine stream:
+//   probe    hash each request's key id into its HBM table (find-or-insert by
+//            CAS), emit the 32-bit slot id as sort key, and accumulate the
+//            radix histograms of every sort pass (fused)
+//   sort     P one-sweep LSD radix passes (rl_sort.h): requests grouped by
+//            slot, arrival order kept
+//   segments one head per distinct slot -> unordered segment list
+//   replay   per segment, the reference's per-request semantics in arrival
+//            order, state gathered once and scattered once (rl_replay.h)
+// Reference boundary replaced: go-redis Eval + Redis Lua + the Go arithmetic
+// around it (tokenbucket.go:90-193, slidingwindow.go:68-185,
+// fixedwindow.go:65-163); see include/rl_engine.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rl_engine.h"
+#include "rl_replay.h"
+#include "rl_semantics.h"
+#include "rl_sort.h"
+#include "rl_table.h"
+
+using namespace rl;
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+
+__global__ void k_init_tb(TbEntry* t, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        t[i].key = EMPTY_KEY;
+        t[i].tok = 0.0;
+        t[i].last = 0.0;
+        t[i].when = ABSENT;
+    }
+}
+
+__global__ void k_init_win(WinEntry* t, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        t[i].key = EMPTY_KEY;
+        t[i].pad = 0;
+        for (int k = 0; k < 2; k++) { t[i].s[k].ws = 0; t[i].s[k].cnt = 0; t[i].s[k].when = ABSENT; }
+    }
+}
+
+constexpr int PROBE_BLOCK = 256;
+
+// find-or-insert every request's key; sort key = global slot id; fused
+// per-pass digit histograms (LDS, then one global atomic per bin per block)
+__global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
+    uint32_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ n,
+    const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
+    uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
+    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, ReqArgs a, uint32_t* eflags) {
+    __shared__ uint32_t lh[4][RADIX];
+    for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t ef = 0;
+    for (uint32_t i = blockIdx.x * PROBE_BLOCK + threadIdx.x; i < m; i += gridDim.x * PROBE_BLOCK) {
+        uint64_t k = key[i];
+        uint32_t c = cfg[i];
+        int64_t nn = n[i];
+        uint32_t slot = invalid_key;
+        bool ok = c < ncfg && nn > 0 && k != EMPTY_KEY;
+        if (k == EMPTY_KEY) ef |= EF_BAD_KEY;
+        if (ok) {
+            int32_t alg = cfgs[c].alg;
+            if (alg == ALG_TOKEN_BUCKET) {
+                uint32_t s = probe_insert(tb, tb_mask, k);
+                if (s == NO_SLOT) ef |= EF_TABLE_FULL; else slot = s;
+            } else {
+                uint32_t s = probe_insert(win, win_mask, k);
+                if (s == NO_SLOT) ef |= EF_TABLE_FULL; else slot = win_base + s;
+            }
+        }
+        if (slot == invalid_key) {
+            a.dec[i] = DEC_INVALID;
+            a.rem[i] = 0;
+            a.retry[i] = 0;
+            a.reset[i] = 0;
+            if (a.tok) a.tok[i] = 0.0;
+        }
+        sk[i] = slot;
+        for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
+    }
+    if (ef) atomicOr(eflags, ef);
+    __syncthreads();
+    for (int p = 0; p < passes; p++) {
+        uint32_t v = lh[p][threadIdx.x];
+        if (v) atomicAdd(&ghist[p * RADIX + threadIdx.x], v);
+    }
+}
+
+// segment heads: one entry per distinct slot (unordered list)
+__global__ __launch_bounds__(256) void k_heads(const uint32_t* __restrict__ sk, uint32_t m,
+                                               uint32_t invalid_key, uint32_t* __restrict__ seg_start,
+                                               uint32_t* nseg) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        uint32_t k = sk[i];
+        bool head = k != invalid_key && (i == 0 || sk[i - 1] != k);
+        if (head) {
+            uint32_t u = atomicAdd(nseg, 1u);
+            seg_start[u] = i;
+        }
+    }
+}
+
+// Reset: DEL of the key(s) AllowN would touch at ts (tokenbucket.go:136-144,
+// slidingwindow.go:125-139, fixedwindow.go:118-128)
+__global__ void k_reset(uint64_t key, int64_t ts, const CfgDev* cfgs, uint32_t cfg, TbEntry* tb,
+                        uint64_t tb_mask, WinEntry* win, uint64_t win_mask) {
+    const CfgDev& c = cfgs[cfg];
+    if (c.alg == ALG_TOKEN_BUCKET) {
+        uint32_t s = probe_find(tb, tb_mask, key);
+        if (s != NO_SLOT) tb[s].when = ABSENT;
+        return;
+    }
+    uint32_t s = probe_find(win, win_mask, key);
+    if (s == NO_SLOT) return;
+    int64_t ws = window_start(ts, c);
+    int64_t pws = ws - c.ttl_c;
+    for (int k = 0; k < 2; k++) {
+        if (win[s].s[k].when == ABSENT) continue;
+        if (win[s].s[k].ws == ws || (c.alg == ALG_SLIDING_WINDOW && win[s].s[k].ws == pws))
+            win[s].s[k].when = ABSENT;
+    }
+}
+
+__global__ void k_q14(const double* in, double* out, uint32_t n) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = rlq::q14(in[i]);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+
+namespace {
+
+constexpr int NSTAGES = 4;
+constexpr uint32_t CTRL_HIST = 0;              // [4][256]
+constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
+constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // segment count
+constexpr uint32_t CTRL_WORDS = CTRL_NSEG + 4;
+
+uint64_t pow2_at_least(uint64_t v) {
+    uint64_t p = 1;
+    while (p < v) p <<= 1;
+    return p;
+}
+int bitlen(uint64_t v) {
+    int b = 0;
+    while (v) { b++; v >>= 1; }
+    return b;
+}
+
+}  // namespace
+
+struct rl_engine {
+    int device = 0;
+    int32_t profile = PROFILE_REDIS7;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    std::vector<CfgDev> h_cfg;
+    CfgDev* d_cfg = nullptr;
+    uint32_t cfg_cap = 0;
+
+    TbEntry* d_tb = nullptr;
+    uint64_t tb_cap = 0;
+    WinEntry* d_win = nullptr;
+    uint64_t win_cap = 0;
+    uint32_t win_base = 0, invalid_key = 0;
+    int sort_bits = 0, sort_passes = 0;
+
+    uint32_t max_batch = 0;
+    uint32_t max_tiles = 0;
+    uint32_t *d_sk0 = nullptr, *d_sk1 = nullptr, *d_sv0 = nullptr, *d_sv1 = nullptr;
+    uint32_t* d_seg = nullptr;
+    uint32_t* d_zero = nullptr;  // ctrl words + look-back status (memset per batch)
+    size_t zero_bytes = 0;
+    uint32_t* d_ctrl = nullptr;
+    uint32_t* d_status = nullptr;
+    uint32_t* d_eflags = nullptr;
+
+    // host-API staging (device side)
+    uint64_t* d_key = nullptr;
+    int64_t *d_ts = nullptr, *d_n = nullptr, *d_sms = nullptr;
+    uint32_t* d_cfgid = nullptr;
+    uint8_t* d_dec = nullptr;
+    int64_t *d_rem = nullptr, *d_retry = nullptr, *d_reset = nullptr;
+    double* d_tok = nullptr;
+
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, NSTAGES + 1>> ev_pending;
+    double stage_ms[NSTAGES] = {0, 0, 0, 0};
+    uint64_t timed_batches = 0;
+
+    rl_stats stats{};
+};
+
+static int fail(rl_engine* e, int code, const std::string& msg) {
+    if (e) e->err = msg;
+    return code;
+}
+
+#define HIPCHK(e, call)                                                                  \
+    do {                                                                                 \
+        hipError_t _st = (call);                                                         \
+        if (_st != hipSuccess)                                                           \
+            return fail((e), RL_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_st)); \
+    } while (0)
+
+static void free_all(rl_engine* e) {
+    (void)hipFree(e->d_cfg);
+    (void)hipFree(e->d_tb);
+    (void)hipFree(e->d_win);
+    (void)hipFree(e->d_sk0); (void)hipFree(e->d_sk1); (void)hipFree(e->d_sv0); (void)hipFree(e->d_sv1);
+    (void)hipFree(e->d_seg);
+    (void)hipFree(e->d_zero);
+    (void)hipFree(e->d_eflags);
+    (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
+    (void)hipFree(e->d_dec); (void)hipFree(e->d_rem); (void)hipFree(e->d_retry); (void)hipFree(e->d_reset); (void)hipFree(e->d_tok);
+    for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
+    if (!o || !out) return RL_EINVAL;
+    *out = nullptr;
+    if (o->profile != PROFILE_REDIS7 && o->profile != PROFILE_MINIREDIS) return RL_EINVAL;
+    if (o->max_batch == 0 || o->max_batch > (1u << 28)) return RL_EINVAL;
+    rl_engine* e = new rl_engine();
+    e->device = o->device;
+    e->profile = o->profile;
+    e->tb_cap = pow2_at_least(std::max<uint64_t>(o->tb_capacity, 1024));
+    e->win_cap = pow2_at_least(std::max<uint64_t>(o->win_capacity, 1024));
+    if (e->tb_cap + e->win_cap >= (1ull << 31)) { delete e; return RL_EINVAL; }
+    e->win_base = (uint32_t)e->tb_cap;
+    e->invalid_key = (uint32_t)(e->tb_cap + e->win_cap);
+    e->sort_bits = bitlen(e->invalid_key);
+    e->sort_passes = (e->sort_bits + 7) / 8;
+    e->max_batch = o->max_batch;
+    e->max_tiles = (o->max_batch + SORT_TILE - 1) / SORT_TILE;
+
+    auto bail = [&](int code) { int r = code; free_all(e); delete e; return r; };
+    if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    size_t M = e->max_batch;
+    e->cfg_cap = 64;
+    bool ok = true;
+    ok &= hipMalloc(&e->d_cfg, sizeof(CfgDev) * e->cfg_cap) == hipSuccess;
+    ok &= hipMalloc(&e->d_tb, sizeof(TbEntry) * e->tb_cap) == hipSuccess;
+    ok &= hipMalloc(&e->d_win, sizeof(WinEntry) * e->win_cap) == hipSuccess;
+    ok &= hipMalloc(&e->d_sk0, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_sk1, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_sv0, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_sv1, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_seg, 4 * M) == hipSuccess;
+    e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
+    ok &= hipMalloc(&e->d_zero, e->zero_bytes) == hipSuccess;
+    ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
+    ok &= hipMalloc(&e->d_key, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_ts, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_n, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_sms, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_cfgid, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_dec, M) == hipSuccess;
+    ok &= hipMalloc(&e->d_rem, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_retry, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_reset, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_tok, 8 * M) == hipSuccess;
+    if (!ok) return bail(RL_ENOMEM);
+    e->d_ctrl = e->d_zero;
+    e->d_status = e->d_zero + CTRL_WORDS;
+    k_init_tb<<<2048, 256, 0, e->stream>>>(e->d_tb, e->tb_cap);
+    k_init_win<<<2048, 256, 0, e->stream>>>(e->d_win, e->win_cap);
+    if (hipMemsetAsync(e->d_eflags, 0, 4, e->stream) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
+    e->stats.sort_bits = e->sort_bits;
+    e->stats.sort_passes = e->sort_passes;
+    *out = e;
+    return RL_OK;
+}
+
+extern "C" int rl_engine_destroy(rl_engine* e) {
+    if (!e) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    free_all(e);
+    delete e;
+    return RL_OK;
+}
+
+extern "C" int rl_config_register(rl_engine* e, uint8_t alg, int64_t limit, int64_t window_ns,
+                                  uint32_t* cfg_id) {
+    if (!e || !cfg_id) return RL_EINVAL;
+    // Validate (config.go:16-50)
+    if (alg < RL_ALG_TOKEN_BUCKET || alg > RL_ALG_FIXED_WINDOW) return fail(e, RL_EINVAL, "unknown algorithm");
+    if (limit <= 0) return fail(e, RL_EINVAL, "limit must be greater than 0");
+    if (window_ns <= 0) return fail(e, RL_EINVAL, "window must be greater than 0");
+    if (window_ns < 1000000LL) return fail(e, RL_EINVAL, "window too small");
+    if (window_ns > 365LL * 24 * 3600 * NS_PER_S) return fail(e, RL_EINVAL, "window too large");
+    CfgDev c = make_cfg(alg, limit, window_ns);
+    (void)hipSetDevice(e->device);
+    if (e->h_cfg.size() == e->cfg_cap) {
+        CfgDev* nd = nullptr;
+        HIPCHK(e, hipMalloc(&nd, sizeof(CfgDev) * e->cfg_cap * 2));
+        HIPCHK(e, hipMemcpyAsync(nd, e->d_cfg, sizeof(CfgDev) * e->cfg_cap, hipMemcpyDeviceToDevice, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        (void)hipFree(e->d_cfg);
+        e->d_cfg = nd;
+        e->cfg_cap *= 2;
+    }
+    e->h_cfg.push_back(c);
+    uint32_t id = (uint32_t)(e->h_cfg.size() - 1);
+    HIPCHK(e, hipMemcpyAsync(e->d_cfg + id, &e->h_cfg[id], sizeof(CfgDev), hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    *cfg_id = id;
+    return RL_OK;
+}
+
+static hipEvent_t take_event(rl_engine* e) {
+    if (!e->ev_pool.empty()) {
+        hipEvent_t ev = e->ev_pool.back();
+        e->ev_pool.pop_back();
+        return ev;
+    }
+    hipEvent_t ev;
+    (void)hipEventCreate(&ev);
+    return ev;
+}
+
+// enqueue one launch sequence for m <= max_batch requests
+static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) {
+    if (m == 0) return RL_OK;
+    std::array<hipEvent_t, NSTAGES + 1> ev{};
+    if (e->timing) {
+        for (auto& x : ev) x = take_event(e);
+        (void)hipEventRecord(ev[0], s);
+    }
+    HIPCHK(e, hipMemsetAsync(e->d_zero, 0, e->zero_bytes, s));
+    uint32_t* ghist = e->d_ctrl + CTRL_HIST;
+    int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, 4096);
+    k_probe<<<probe_grid, PROBE_BLOCK, 0, s>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
+                                                e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
+                                                e->win_base, e->invalid_key, e->d_sk0, ghist,
+                                                e->sort_passes, a, e->d_eflags);
+    if (e->timing) (void)hipEventRecord(ev[1], s);
+    uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
+    uint32_t *kin = e->d_sk0, *vin = e->d_sv0, *kout = e->d_sk1, *vout = e->d_sv1;
+    for (int p = 0; p < e->sort_passes; p++) {
+        uint32_t* status = e->d_status + (size_t)p * e->max_tiles * RADIX;
+        if (p == 0)
+            k_sort_pass<true><<<tiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
+                                                           status, e->d_ctrl + CTRL_TILE + p, e->d_eflags);
+        else
+            k_sort_pass<false><<<tiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
+                                                            status, e->d_ctrl + CTRL_TILE + p, e->d_eflags);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+    }
+    if (e->timing) (void)hipEventRecord(ev[2], s);
+    // sorted keys/values are now in kin/vin
+    uint32_t* nseg = e->d_ctrl + CTRL_NSEG;
+    int grid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
+    k_heads<<<grid, 256, 0, s>>>(kin, m, e->invalid_key, e->d_seg, nseg);
+    if (e->timing) (void)hipEventRecord(ev[3], s);
+    k_replay_serial<<<grid, 256, 0, s>>>(kin, vin, m, e->d_seg, nseg, e->win_base, e->d_tb, e->d_win,
+                                         e->d_cfg, e->profile, a, e->d_eflags);
+    if (e->timing) {
+        (void)hipEventRecord(ev[4], s);
+        e->ev_pending.push_back(ev);
+    }
+    HIPCHK(e, hipGetLastError());
+    e->stats.batches++;
+    e->stats.decisions += m;
+    return RL_OK;
+}
+
+static int check_flags(rl_engine* e, uint32_t f) {
+    if (f & EF_TABLE_FULL) return fail(e, RL_ENOMEM, "state table full");
+    if (f & EF_LOOKBACK) return fail(e, RL_ETIMEOUT, "radix sort look-back timed out");
+    if (f & EF_ORDER) return fail(e, RL_EORDER, "per-key window ids went backwards");
+    return RL_OK;
+}
+
+extern "C" int rl_engine_sync(rl_engine* e) {
+    if (!e) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipDeviceSynchronize());
+    uint32_t f = 0;
+    HIPCHK(e, hipMemcpy(&f, e->d_eflags, 4, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemset(e->d_eflags, 0, 4));
+    return check_flags(e, f);
+}
+
+extern "C" int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
+                                      const int64_t* n, const uint32_t* cfg_id, const int64_t* server_ms,
+                                      uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                                      int64_t* reset_at_ns, double* tokens, void* stream) {
+    if (!e || (m && (!key_id || !ts_ns || !n || !cfg_id || !decision || !remaining || !retry_after_ns || !reset_at_ns)))
+        return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    for (size_t off = 0; off < m; off += e->max_batch) {
+        uint32_t c = (uint32_t)std::min<size_t>(e->max_batch, m - off);
+        ReqArgs a{key_id + off, ts_ns + off, n + off, cfg_id + off, server_ms ? server_ms + off : nullptr,
+                  decision + off, remaining + off, retry_after_ns + off, reset_at_ns + off,
+                  tokens ? tokens + off : nullptr};
+        int r = run_batch(e, c, a, s);
+        if (r != RL_OK) return r;
+    }
+    return RL_OK;
+}
+
+extern "C" int rl_decide_batch(rl_engine* e, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
+                               const int64_t* n, const uint32_t* cfg_id, const int64_t* server_ms,
+                               uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                               int64_t* reset_at_ns, double* tokens) {
+    if (!e || (m && (!key_id || !ts_ns || !n || !cfg_id || !decision || !remaining || !retry_after_ns || !reset_at_ns)))
+        return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = e->stream;
+    HIPCHK(e, hipMemsetAsync(e->d_eflags, 0, 4, s));
+    for (size_t off = 0; off < m; off += e->max_batch) {
+        uint32_t c = (uint32_t)std::min<size_t>(e->max_batch, m - off);
+        HIPCHK(e, hipMemcpyAsync(e->d_key, key_id + off, 8 * (size_t)c, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipMemcpyAsync(e->d_ts, ts_ns + off, 8 * (size_t)c, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipMemcpyAsync(e->d_n, n + off, 8 * (size_t)c, hipMemcpyHostToDevice, s));
+        HIPCHK(e, hipMemcpyAsync(e->d_cfgid, cfg_id + off, 4 * (size_t)c, hipMemcpyHostToDevice, s));
+        if (server_ms) HIPCHK(e, hipMemcpyAsync(e->d_sms, server_ms + off, 8 * (size_t)c, hipMemcpyHostToDevice, s));
+        ReqArgs a{e->d_key, e->d_ts, e->d_n, e->d_cfgid, server_ms ? e->d_sms : nullptr,
+                  e->d_dec, e->d_rem, e->d_retry, e->d_reset, tokens ? e->d_tok : nullptr};
+        int r = run_batch(e, c, a, s);
+        if (r != RL_OK) return r;
+        HIPCHK(e, hipMemcpyAsync(decision + off, e->d_dec, c, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipMemcpyAsync(remaining + off, e->d_rem, 8 * (size_t)c, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipMemcpyAsync(retry_after_ns + off, e->d_retry, 8 * (size_t)c, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipMemcpyAsync(reset_at_ns + off, e->d_reset, 8 * (size_t)c, hipMemcpyDeviceToHost, s));
+        if (tokens) HIPCHK(e, hipMemcpyAsync(tokens + off, e->d_tok, 8 * (size_t)c, hipMemcpyDeviceToHost, s));
+        HIPCHK(e, hipStreamSynchronize(s));
+    }
+    uint32_t f = 0;
+    HIPCHK(e, hipMemcpy(&f, e->d_eflags, 4, hipMemcpyDeviceToHost));
+    return check_flags(e, f);
+}
+
+extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns) {
+    if (!e || cfg_id >= e->h_cfg.size() || key_id == EMPTY_KEY) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    k_reset<<<1, 1, 0, e->stream>>>(key_id, ts_ns, e->d_cfg, cfg_id, e->d_tb, e->tb_cap - 1, e->d_win,
+                                     e->win_cap - 1);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return RL_OK;
+}
+
+extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
+    if (!e || !out) return RL_EINVAL;
+    *out = e->stats;
+    return RL_OK;
+}
+
+extern "C" int rl_engine_set_timing(rl_engine* e, int on) {
+    if (!e) return RL_EINVAL;
+    e->timing = on != 0;
+    return RL_OK;
+}
+
+extern "C" int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint64_t* batches) {
+    if (!e) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    for (auto& ev : e->ev_pending) {
+        HIPCHK(e, hipEventSynchronize(ev[NSTAGES]));
+        for (int k = 0; k < NSTAGES; k++) {
+            float t = 0;
+            HIPCHK(e, hipEventElapsedTime(&t, ev[k], ev[k + 1]));
+            e->stage_ms[k] += t;
+        }
+        e->timed_batches++;
+        for (auto x : ev) e->ev_pool.push_back(x);
+    }
+    e->ev_pending.clear();
+    for (int k = 0; k < nstages && k < NSTAGES; k++) ms[k] = e->stage_ms[k];
+    if (batches) *batches = e->timed_batches;
+    for (int k = 0; k < NSTAGES; k++) e->stage_ms[k] = 0;
+    e->timed_batches = 0;
+    return RL_OK;
+}
+
+extern "C" int rl_last_error(rl_engine* e, char* buf, size_t len) {
+    if (!e || !buf || !len) return RL_EINVAL;
+    snprintf(buf, len, "%s", e->err.c_str());
+    return RL_OK;
+}
+
+extern "C" int rl_selftest_q14_host(const double* in, double* out, size_t n) {
+    if (!in || !out) return RL_EINVAL;
+    for (size_t i = 0; i < n; i++) out[i] = rlq::q14(in[i]);
+    return RL_OK;
+}
+
+extern "C" int rl_selftest_q14_device(rl_engine* e, const double* in, double* out, size_t n) {
+    if (!e || !in || !out) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    double *di = nullptr, *dout = nullptr;
+    HIPCHK(e, hipMalloc(&di, 8 * std::max<size_t>(n, 1)));
+    HIPCHK(e, hipMalloc(&dout, 8 * std::max<size_t>(n, 1)));
+    HIPCHK(e, hipMemcpy(di, in, 8 * n, hipMemcpyHostToDevice));
+    if (n) k_q14<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(di, dout, (uint32_t)n);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(out, dout, 8 * n, hipMemcpyDeviceToHost));
+    (void)hipFree(di);
+    (void)hipFree(dout);
+    return RL_OK;
+}

@@ -1,0 +1,349 @@
+"""ctypes binding of the MI355X rate-limit engine (include/rl_engine.h) and of
+its host mirror of the reference Go API (include/rl_limiter.h).
+
+This is plumbing for tests and bench.py: the product is the HIP library
+lib/librl_amd.so.  There is no CPU fallback: if the library is missing,
+importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librl_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"HIP engine library not built: {LIB_PATH} (run `make -C distributed-rate-limiter_amd` "
+        "or __graft_entry__.build())"
+    )
+lib = C.CDLL(LIB_PATH)
+
+# --- constants (include/rl_engine.h) -----------------------------------------
+RL_OK, RL_EINVAL, RL_ENOMEM, RL_EDEVICE, RL_ETIMEOUT, RL_EORDER = 0, -22, -12, -5, -110, -34
+TOKEN_BUCKET, SLIDING_WINDOW, FIXED_WINDOW = 1, 2, 3
+ALG_BY_NAME = {"token_bucket": TOKEN_BUCKET, "sliding_window": SLIDING_WINDOW, "fixed_window": FIXED_WINDOW}
+PROFILE_REDIS7, PROFILE_MINIREDIS = 0, 1
+DENIED, ALLOWED, ERROR, INVALID = 0, 1, 2, 3
+KEY_RESERVED = (1 << 64) - 1
+
+RLL_OK, RLL_ERR_INVALID_N, RLL_ERR_FAILED, RLL_ERR_CONFIG, RLL_ERR_RESET, RLL_ERR_ARG = 0, 1, 2, 3, 4, 5
+NOW_WALL = -(1 << 63)
+SMS_DEFAULT = -(1 << 63)
+
+
+class rl_opts(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("profile", C.c_int32),
+        ("tb_capacity", C.c_uint64),
+        ("win_capacity", C.c_uint64),
+        ("max_batch", C.c_uint32),
+        ("flags", C.c_uint32),
+    ]
+
+
+class rl_stats(C.Structure):
+    _fields_ = [
+        ("batches", C.c_uint64),
+        ("decisions", C.c_uint64),
+        ("last_segments", C.c_uint64),
+        ("last_heavy", C.c_uint64),
+        ("sort_bits", C.c_uint32),
+        ("sort_passes", C.c_uint32),
+    ]
+
+
+class rll_result(C.Structure):
+    _fields_ = [
+        ("allowed", C.c_uint8),
+        ("limit", C.c_int64),
+        ("remaining", C.c_int64),
+        ("retry_after_ns", C.c_int64),
+        ("reset_at_ns", C.c_int64),
+    ]
+
+
+vp = C.c_void_p
+_sig = {
+    "rl_engine_create": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp)]),
+    "rl_engine_destroy": (C.c_int, [vp]),
+    "rl_config_register": (C.c_int, [vp, C.c_uint8, C.c_int64, C.c_int64, C.POINTER(C.c_uint32)]),
+    "rl_decide_batch": (C.c_int, [vp, C.c_size_t] + [vp] * 10),
+    "rl_decide_batch_device": (C.c_int, [vp, C.c_size_t] + [vp] * 11),
+    "rl_engine_sync": (C.c_int, [vp]),
+    "rl_reset": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_int64]),
+    "rl_engine_stats": (C.c_int, [vp, C.POINTER(rl_stats)]),
+    "rl_engine_set_timing": (C.c_int, [vp, C.c_int]),
+    "rl_engine_stage_times": (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_uint64)]),
+    "rl_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
+    "rl_selftest_q14_host": (C.c_int, [vp, vp, C.c_size_t]),
+    "rl_selftest_q14_device": (C.c_int, [vp, vp, vp, C.c_size_t]),
+    "rll_engine_new": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp), C.c_char_p, C.c_size_t]),
+    "rll_engine_free": (C.c_int, [vp]),
+    "rll_engine_raw": (vp, [vp]),
+    "rll_engine_set_server_ms": (C.c_int, [vp, C.c_int64]),
+    "rll_config_validate": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_char_p, C.c_size_t]),
+    "rll_format_key": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "rll_duration_string": (C.c_int, [C.c_int64, C.c_char_p, C.c_size_t]),
+    "rll_new": (C.c_int, [vp, C.c_char_p, C.c_int64, C.c_int64, C.c_char_p, C.c_int, C.c_int,
+                          C.POINTER(vp), C.c_char_p, C.c_size_t]),
+    "rll_allow_n": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int64, C.c_int64, C.c_int,
+                              C.POINTER(rll_result), C.c_char_p, C.c_size_t]),
+    "rll_allow_batch": (C.c_int, [vp, C.c_size_t, vp, vp, vp, vp, vp, vp]),
+    "rll_reset": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int64, C.c_char_p, C.c_size_t]),
+    "rll_close": (C.c_int, [vp]),
+    "rll_free": (C.c_int, [vp]),
+}
+for _name, (_res, _args) in _sig.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(vp)
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (status {code})")
+        self.code = code
+
+
+def q14_host(x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    lib.rl_selftest_q14_host(_ptr(x), _ptr(out), x.size)
+    return out
+
+
+@dataclass
+class Decisions:
+    decision: np.ndarray
+    remaining: np.ndarray
+    retry_after_ns: np.ndarray
+    reset_at_ns: np.ndarray
+    tokens: np.ndarray | None
+
+
+class Engine:
+    """rl_engine: the batched decision engine on one GPU."""
+
+    def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
+                 max_batch=1 << 20, device=0):
+        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, 0)
+        h = vp()
+        rc = lib.rl_engine_create(C.byref(o), C.byref(h))
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_engine_create failed")
+        self.h = h
+        self.profile = profile
+
+    def close(self):
+        if self.h:
+            lib.rl_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self) -> str:
+        buf = C.create_string_buffer(512)
+        lib.rl_last_error(self.h, buf, 512)
+        return buf.value.decode()
+
+    def register(self, alg: int, limit: int, window_ns: int) -> int:
+        cid = C.c_uint32()
+        rc = lib.rl_config_register(self.h, alg, limit, window_ns, C.byref(cid))
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+        return cid.value
+
+    def decide(self, key, ts, n, cfg, server_ms=None, want_tokens=True, check=True) -> Decisions:
+        key = np.ascontiguousarray(key, dtype=np.uint64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        n = np.ascontiguousarray(n, dtype=np.int64)
+        cfg = np.ascontiguousarray(cfg, dtype=np.uint32)
+        sms = None if server_ms is None else np.ascontiguousarray(server_ms, dtype=np.int64)
+        m = key.size
+        out = Decisions(np.empty(m, np.uint8), np.empty(m, np.int64), np.empty(m, np.int64),
+                        np.empty(m, np.int64), np.empty(m, np.float64) if want_tokens else None)
+        rc = lib.rl_decide_batch(self.h, m, _ptr(key), _ptr(ts), _ptr(n), _ptr(cfg), _ptr(sms),
+                                 _ptr(out.decision), _ptr(out.remaining), _ptr(out.retry_after_ns),
+                                 _ptr(out.reset_at_ns), _ptr(out.tokens))
+        if check and rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+        out.status = rc
+        return out
+
+    def decide_device(self, m, key_p, ts_p, n_p, cfg_p, sms_p, dec_p, rem_p, retry_p, reset_p, tok_p,
+                      stream=None):
+        rc = lib.rl_decide_batch_device(self.h, m, key_p, ts_p, n_p, cfg_p, sms_p, dec_p, rem_p,
+                                        retry_p, reset_p, tok_p, stream)
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+
+    def sync(self) -> int:
+        return lib.rl_engine_sync(self.h)
+
+    def reset(self, cfg: int, key: int, ts: int):
+        rc = lib.rl_reset(self.h, cfg, key, ts)
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+
+    def stats(self) -> rl_stats:
+        s = rl_stats()
+        lib.rl_engine_stats(self.h, C.byref(s))
+        return s
+
+    def set_timing(self, on: bool):
+        lib.rl_engine_set_timing(self.h, 1 if on else 0)
+
+    def stage_times(self):
+        ms = np.zeros(4, np.float64)
+        nb = C.c_uint64()
+        lib.rl_engine_stage_times(self.h, _ptr(ms), 4, C.byref(nb))
+        return ms, nb.value
+
+    def q14_device(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.empty_like(x)
+        rc = lib.rl_selftest_q14_device(self.h, _ptr(x), _ptr(out), x.size)
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+        return out
+
+
+# --- host mirror of the Go API (include/rl_limiter.h) ------------------------
+
+def config_validate(algorithm, limit, window_ns):
+    """Config.Validate(); algorithm None == nil *Config.  Returns '' or the message."""
+    buf = C.create_string_buffer(512)
+    a = None if algorithm is None else algorithm.encode()
+    rc = lib.rll_config_validate(a, limit, window_ns, buf, 512)
+    return "" if rc == RLL_OK else buf.value.decode()
+
+
+def format_key(prefix, key):
+    buf = C.create_string_buffer(4096)
+    lib.rll_format_key(None if prefix is None else prefix.encode(), key.encode(), buf, 4096)
+    return buf.value.decode()
+
+
+def duration_string(d):
+    buf = C.create_string_buffer(64)
+    lib.rll_duration_string(d, buf, 64)
+    return buf.raw.split(b"\0", 1)[0].decode("utf-8")
+
+
+@dataclass
+class Result:
+    Allowed: bool
+    Limit: int
+    Remaining: int
+    RetryAfter: int
+    ResetAt: int
+
+
+class GoError(Exception):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+        self.msg = msg
+
+
+class LimiterEngine:
+    """rll_engine: one GPU engine + key interner shared by limiters."""
+
+    def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
+                 max_batch=1 << 16, device=0):
+        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, 0)
+        h = vp()
+        buf = C.create_string_buffer(512)
+        rc = lib.rll_engine_new(C.byref(o), C.byref(h), buf, 512)
+        if rc != RLL_OK:
+            raise GoError(rc, buf.value.decode())
+        self.h = h
+
+    def set_server_ms(self, ms):
+        lib.rll_engine_set_server_ms(self.h, SMS_DEFAULT if ms is None else ms)
+
+    def close(self):
+        if self.h:
+            lib.rll_engine_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class RateLimiter:
+    """Mirror of the reference RateLimiter (interface.go:76-145)."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def allow(self, key, now_ns=NOW_WALL, cancelled=False):
+        return self.allow_n(key, 1, now_ns, cancelled)
+
+    def allow_n(self, key, n, now_ns=NOW_WALL, cancelled=False):
+        """Returns (Result | None, error message | None, code)."""
+        r = rll_result()
+        buf = C.create_string_buffer(512)
+        kb = key.encode()
+        rc = lib.rll_allow_n(self.h, kb, len(kb), n, now_ns, 1 if cancelled else 0, C.byref(r), buf, 512)
+        if rc == RLL_OK:
+            return Result(bool(r.allowed), r.limit, r.remaining, r.retry_after_ns, r.reset_at_ns), None, rc
+        return None, buf.value.decode(), rc
+
+    def batch_allow(self, keys, n, now_ns=None):
+        m = len(keys)
+        kbs = [k.encode() for k in keys]
+        arr = (C.c_char_p * m)(*kbs)
+        lens = np.array([len(k) for k in kbs], np.uint64)
+        nn = np.ascontiguousarray(n, np.int64)
+        now = None if now_ns is None else np.ascontiguousarray(now_ns, np.int64)
+        out = (rll_result * m)()
+        codes = np.empty(m, np.int32)
+        lib.rll_allow_batch(self.h, m, C.cast(arr, vp), _ptr(lens), _ptr(nn), _ptr(now), C.cast(out, vp),
+                            _ptr(codes))
+        res = [Result(bool(o.allowed), o.limit, o.remaining, o.retry_after_ns, o.reset_at_ns) for o in out]
+        return res, codes
+
+    def reset(self, key, now_ns=NOW_WALL):
+        buf = C.create_string_buffer(512)
+        kb = key.encode()
+        rc = lib.rll_reset(self.h, kb, len(kb), now_ns, buf, 512)
+        return None if rc == RLL_OK else buf.value.decode()
+
+    def close(self):
+        lib.rll_close(self.h)
+
+    def __del__(self):
+        try:
+            lib.rll_free(self.h)
+        except Exception:
+            pass
+
+
+def new_limiter(engine: LimiterEngine | None, algorithm, limit, window_ns, prefix="", fail_open=False,
+                config_nil=False):
+    """NewTokenBucket/NewSlidingWindow/NewFixedWindow by name; raises GoError like the constructor."""
+    h = vp()
+    buf = C.create_string_buffer(512)
+    rc = lib.rll_new(None if engine is None else engine.h, algorithm.encode(), limit, window_ns,
+                     prefix.encode(), 1 if fail_open else 0, 1 if config_nil else 0, C.byref(h), buf, 512)
+    if rc != RLL_OK:
+        raise GoError(rc, buf.value.decode())
+    return RateLimiter(h)

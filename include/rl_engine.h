@@ -1,0 +1,132 @@
+/*
+ * rl_engine.h -- C-ABI of the MI355X batched rate-limit decision engine.
+ *
+ * This is the drop-in boundary that replaces the reference's storage seam:
+ * every decision the reference makes with one go-redis EVAL round trip
+ *   tokenbucket.go:172   client.Eval(ctx, tokenBucketScript, ...)
+ *   slidingwindow.go:164 client.Eval(ctx, slidingWindowScript, ...)
+ *   fixedwindow.go:152   client.Eval(ctx, fixedWindowScript, ...)
+ * plus the Go arithmetic around it (AllowN, tokenbucket.go:90-133,
+ * slidingwindow.go:68-122, fixedwindow.go:65-115) is made here, for a whole
+ * batch, by HIP kernels over an HBM-resident state table.  Reset's DEL
+ * (tokenbucket.go:139, slidingwindow.go:134, fixedwindow.go:123) maps to
+ * rl_reset.  A cgo binding is shown in INTEGRATION.md.
+ *
+ * Conventions: plain C types only; arrays are caller-owned and only accessed
+ * during the call (the *_device entry point: until the stream reaches it); the
+ * engine owns all device memory.  Calls on one engine are not re-entrant.
+ * Every function returns RL_OK (0) or a negative RL_E* status.
+ */
+#ifndef RL_ENGINE_H
+#define RL_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define RL_OK          0
+#define RL_EINVAL    (-22)  /* bad argument / config fails Validate (config.go:16-50) */
+#define RL_ENOMEM    (-12)  /* device allocation failed or state table full */
+#define RL_EDEVICE    (-5)  /* HIP runtime error (text in rl_last_error) */
+#define RL_ETIMEOUT (-110)  /* a device-side bounded wait expired */
+#define RL_EORDER    (-34)  /* per-key window ids went backwards (contract breach) */
+
+/* algorithms (interface.go:11-23) */
+#define RL_ALG_TOKEN_BUCKET   1
+#define RL_ALG_SLIDING_WINDOW 2
+#define RL_ALG_FIXED_WINDOW   3
+
+/* backend semantics profile */
+#define RL_PROFILE_REDIS7    0  /* real Redis 7: Lua tostring "%.14g", expiry now > when */
+#define RL_PROFILE_MINIREDIS 1  /* miniredis + gopher-lua (the reference tests) */
+
+/* per-request decision codes */
+#define RL_DENIED  0
+#define RL_ALLOWED 1
+#define RL_ERROR   2  /* the script failed (INCRBY overflow): Go sees err != nil */
+#define RL_INVALID 3  /* n <= 0, unknown cfg id or reserved key id: not executed */
+
+/* reserved key id (marks an empty table slot) */
+#define RL_KEY_RESERVED UINT64_MAX
+
+typedef struct rl_engine rl_engine;
+
+typedef struct rl_opts {
+    int32_t  device;        /* HIP device ordinal */
+    int32_t  profile;       /* RL_PROFILE_* */
+    uint64_t tb_capacity;   /* token-bucket table slots; rounded up to a power of 2 */
+    uint64_t win_capacity;  /* window-counter table slots; rounded up to a power of 2 */
+    uint32_t max_batch;     /* largest batch one launch sequence handles (<= 2^28) */
+    uint32_t flags;         /* reserved, 0 */
+} rl_opts;
+
+typedef struct rl_stats {
+    uint64_t batches;
+    uint64_t decisions;
+    uint64_t last_segments;   /* distinct keys in the last batch */
+    uint64_t last_heavy;      /* segments replayed cooperatively in the last batch */
+    uint32_t sort_bits;
+    uint32_t sort_passes;
+} rl_stats;
+
+/* replaces redis.NewClient + NewTokenBucket/NewSlidingWindow/NewFixedWindow's
+ * storage (tokenbucket.go:63-81 etc.) */
+int rl_engine_create(const rl_opts* opts, rl_engine** out);
+int rl_engine_destroy(rl_engine* e);
+
+/* Register one limiter config (Config, interface.go:46-70; Validate config.go:16-50).
+ * State is keyed by key_id only: callers give each (config, formatted key)
+ * its own id, as FormatKey(key) is unique per prefix (config.go:81-87). */
+int rl_config_register(rl_engine* e, uint8_t alg, int64_t limit, int64_t window_ns,
+                       uint32_t* cfg_id);
+
+/* One batch in arrival order (array index = seq).  Host arrays; synchronous.
+ *   ts_ns      request time, Unix ns (stands for time.Now() in AllowN)
+ *   n          AllowN count (Allow = 1); n <= 0 yields RL_INVALID
+ *   server_ms  Redis clock per request (nullable: floor(ts_ns / 1e6))
+ * Outputs per request: decision (RL_DENIED/ALLOWED/ERROR/INVALID), remaining,
+ * retry_after_ns, reset_at_ns (Unix ns; also valid for RL_ERROR, for the
+ * fail-open Result), tokens (nullable; token-bucket only: the Lua `tokens`
+ * value at the end of the script, bit-exact). */
+int rl_decide_batch(rl_engine* e, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
+                    const int64_t* n, const uint32_t* cfg_id, const int64_t* server_ms,
+                    uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                    int64_t* reset_at_ns, double* tokens);
+
+/* Same, with device pointers, enqueued on `stream` (a hipStream_t; NULL = the
+ * engine's stream).  Asynchronous: check errors with rl_engine_sync. */
+int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
+                           const int64_t* n, const uint32_t* cfg_id, const int64_t* server_ms,
+                           uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                           int64_t* reset_at_ns, double* tokens, void* stream);
+
+/* wait for queued work; returns the sticky device status (RL_ENOMEM if the
+ * table filled, RL_EORDER, RL_ETIMEOUT) and clears it */
+int rl_engine_sync(rl_engine* e);
+
+/* Reset(ctx, key) at time ts_ns: DEL of the key(s) AllowN would touch at ts_ns */
+int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns);
+
+int rl_engine_stats(rl_engine* e, rl_stats* out);
+
+/* per-stage device time (ms) accumulated since the last call, measured with
+ * HIP events on the stream the kernels run on; stages: 0 probe, 1 sort,
+ * 2 segments, 3 replay.  Requires rl_engine_set_timing(e, 1). */
+int rl_engine_set_timing(rl_engine* e, int on);
+int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint64_t* batches);
+
+int rl_last_error(rl_engine* e, char* buf, size_t len);
+
+/* self-test hooks: exact tonumber(tostring(x)) of Redis Lua ("%.14g"),
+ * host instantiation and device instantiation of the same code */
+int rl_selftest_q14_host(const double* in, double* out, size_t n);
+int rl_selftest_q14_device(rl_engine* e, const double* in, double* out, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

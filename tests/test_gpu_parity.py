@@ -1,0 +1,181 @@
+"""HIP engine vs CPU oracle: bit-exact parity on seeded traces (GPU).
+
+Integer/index outputs (decision, remaining, retry_after_ns, reset_at_ns) must be
+identical; token-bucket `tokens` (the Lua variable at the end of the script)
+must be the identical IEEE double (compared as bit patterns).
+"""
+import numpy as np
+import pytest
+
+import oracle
+import traces
+from tracegen import CONFIG_SETS, T0, NS, random_trace
+
+pytestmark = pytest.mark.gpu
+
+
+def make_engine(rl, profile, tb=1 << 20, win=1 << 20, max_batch=1 << 20):
+    return rl.Engine(profile=profile, tb_capacity=tb, win_capacity=win, max_batch=max_batch)
+
+
+def assert_same(res, ref, configs, cfg, what=""):
+    dec, rem, retry, reset, tok = ref
+    bad = np.nonzero(res.decision != dec)[0]
+    assert bad.size == 0, f"{what} decision mismatch at {bad[:10]}: gpu={res.decision[bad[:10]]} ref={dec[bad[:10]]}"
+    ok = dec != 3
+    for name, a, b in [("remaining", res.remaining, rem), ("retry", res.retry_after_ns, retry),
+                       ("reset_at", res.reset_at_ns, reset)]:
+        bad = np.nonzero((a != b) & ok)[0]
+        assert bad.size == 0, f"{what} {name} mismatch at {bad[:10]}: gpu={a[bad[:10]]} ref={b[bad[:10]]}"
+    if res.tokens is not None:
+        is_tb = np.array([configs[c][0] == 1 if c < len(configs) else False for c in cfg]) & (dec <= 1)
+        gb = res.tokens.view(np.uint64)[is_tb]
+        rb = tok.view(np.uint64)[is_tb]
+        bad = np.nonzero(gb != rb)[0]
+        assert bad.size == 0, f"{what} tokens mismatch: gpu={res.tokens[is_tb][bad[:5]]} ref={tok[is_tb][bad[:5]]}"
+
+
+def run_both(rl, profile, configs, batches, **kw):
+    eng = make_engine(rl, profile, **kw)
+    sim = oracle.OracleSim(profile)
+    for a, L, W in configs:
+        assert eng.register(a, L, W) == sim.add_config(a, L, W)
+    for i, (key, ts, n, cfg, sms) in enumerate(batches):
+        res = eng.decide(key, ts, n, cfg, sms)
+        ref = sim.decide(key, ts, n, cfg, sms)
+        assert_same(res, ref, configs, cfg, what=f"batch {i}")
+    return eng, sim
+
+
+def split(trace, sizes):
+    key, ts, n, cfg, sms = trace
+    out, o = [], 0
+    for s in sizes:
+        out.append((key[o:o + s], ts[o:o + s], n[o:o + s], cfg[o:o + s], None if sms is None else sms[o:o + s]))
+        o += s
+    return out
+
+
+# --- exact %.14g on the device -------------------------------------------------
+
+def test_q14_device_matches_glibc(rl):
+    eng = make_engine(rl, 0, tb=1024, win=1024, max_batch=1024)
+    rng = np.random.default_rng(11)
+    bits = rng.integers(0, 1 << 63, 400_000, dtype=np.int64).astype(np.uint64) | \
+        (rng.integers(0, 2, 400_000).astype(np.uint64) << np.uint64(63))
+    x = bits.view(np.float64)
+    x = x[np.isfinite(x)]
+    x = np.concatenate([x, rng.random(200_000) * 20, rng.random(200_000) * 1e-6,
+                        (T0 + rng.integers(0, 10 ** 11, 200_000)) / 1e9,
+                        [0.0, -0.0, 1.0000610351562500, 0.999999999999995, 5e-324, 1.7e308]])
+    dev = eng.q14_device(x)
+    host = rl.q14_host(x)
+    assert np.array_equal(dev.view(np.uint64), host.view(np.uint64))
+    ref = np.array([float("%.14g" % v) for v in x[::50]])
+    assert np.array_equal(host[::50].view(np.uint64), ref.view(np.uint64))
+
+
+# --- randomized multi-config traces, multiple batches (state carried) ----------
+
+@pytest.mark.parametrize("profile", [0, 1])
+@pytest.mark.parametrize("kind", ["tb", "sw", "fw", "mixed"])
+@pytest.mark.parametrize("ff", [False, True])
+def test_random_traces(rl, profile, kind, ff):
+    configs = CONFIG_SETS[kind]
+    seed = {"tb": 1, "sw": 2, "fw": 3, "mixed": 4}[kind] * 10 + profile * 2 + int(ff)
+    tr = random_trace(seed, 60_000, 500, configs, fastforward=ff, big_n=True)
+    run_both(rl, profile, configs, split(tr, [1, 7, 1000, 9000, 20000, 29992]))
+
+
+def test_hot_keys_long_segments(rl):
+    # a few keys carrying most traffic: long per-key segments in one batch
+    configs = CONFIG_SETS["mixed"]
+    rng = np.random.default_rng(5)
+    m = 200_000
+    key = rng.choice(np.arange(15, dtype=np.uint64), m, p=np.full(15, 1 / 15))
+    ts = T0 + np.cumsum(rng.integers(0, 20_000, m)).astype(np.int64)
+    n = np.ones(m, np.int64)
+    cfg = (key % len(configs)).astype(np.uint32)
+    for profile in (0, 1):
+        run_both(rl, profile, configs, split((key, ts, n, cfg, None), [100_000, 100_000]))
+
+
+# --- BASELINE configs at full batch size ----------------------------------------
+
+def test_config1_tb_zipf_full_batches(rl):
+    g = traces.TokenBucketZipf(batch=1_000_000)
+    run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 21, win=1 << 10)
+
+
+def test_config0_fw_uniform(rl):
+    g = traces.FixedWindowUniform(batch=1_000_000)
+    run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 10, win=1 << 15)
+
+
+def test_config2_sw_bursty(rl):
+    g = traces.SlidingWindowBursty(nkeys=2_000_000, batch=500_000, span_s=180.0, nbatches=4)
+    run_both(rl, 0, g.configs, [g.next_batch() for _ in range(4)], tb=1 << 10, win=1 << 22)
+
+
+def test_config3_mixed(rl):
+    g = traces.MixedTenants(nkeys=300_000, batch=500_000)
+    run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 19, win=1 << 20)
+
+
+# --- edges ----------------------------------------------------------------------
+
+def test_empty_and_invalid(rl):
+    eng = make_engine(rl, 0, tb=1024, win=1024, max_batch=4096)
+    c = eng.register(1, 10, 60 * NS)
+    res = eng.decide(np.zeros(0, np.uint64), np.zeros(0, np.int64), np.zeros(0, np.int64), np.zeros(0, np.uint32))
+    assert res.decision.size == 0
+    key = np.array([1, 2, rl.KEY_RESERVED, 3], np.uint64)
+    res = eng.decide(key, np.full(4, T0), np.array([1, 0, 1, -3]), np.array([c, c, c, 7], np.uint32), check=False)
+    assert list(res.decision) == [1, 3, 3, 3]
+
+
+def test_batches_larger_than_max_batch(rl):
+    configs = CONFIG_SETS["mixed"]
+    tr = random_trace(77, 50_000, 300, configs)
+    eng = make_engine(rl, 0, tb=1 << 12, win=1 << 12, max_batch=4096)   # forces 13 chunks
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    assert_same(eng.decide(*tr[:4]), sim.decide(*tr[:4]), configs, tr[3])
+
+
+def test_reset_between_batches(rl):
+    configs = CONFIG_SETS["mixed"]
+    tr = random_trace(78, 20_000, 50, configs)
+    eng = make_engine(rl, 0, tb=1 << 12, win=1 << 12)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    for part in split(tr, [5000, 5000, 5000, 5000]):
+        assert_same(eng.decide(*part[:4]), sim.decide(*part[:4]), configs, part[3])
+        t = int(part[1][-1])
+        for k in range(0, 50, 3):
+            eng.reset(k % len(configs), k, t)
+            sim.reset(k % len(configs), k, t)
+
+
+def test_table_full_is_reported(rl):
+    eng = make_engine(rl, 0, tb=1024, win=1024, max_batch=4096)
+    c = eng.register(1, 10, 60 * NS)
+    key = np.arange(2000, dtype=np.uint64)
+    res = eng.decide(key, np.full(2000, T0), np.ones(2000, np.int64), np.full(2000, c, np.uint32), check=False)
+    assert res.status == rl.RL_ENOMEM
+
+
+def test_deterministic_repeat(rl):
+    g1, g2 = traces.TokenBucketZipf(batch=200_000), traces.TokenBucketZipf(batch=200_000)
+    outs = []
+    for g in (g1, g2):
+        eng = make_engine(rl, 0, tb=1 << 21, win=1024)
+        eng.register(*g.configs[0])
+        outs.append([eng.decide(*g.next_batch()) for _ in range(2)])
+    for a, b in zip(*outs):
+        assert np.array_equal(a.decision, b.decision)
+        assert np.array_equal(a.tokens.view(np.uint64), b.tokens.view(np.uint64))

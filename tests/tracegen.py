@@ -1,0 +1,33 @@
+"""Seeded adversarial traces for parity tests (both the CPU oracle cross-check
+and the GPU parity tests use these)."""
+import numpy as np
+
+NS = 1_000_000_000
+T0 = 1_760_000_000_000_000_000
+
+CONFIG_SETS = {
+    "tb": [(1, 20, 12 * NS), (1, 5, 60 * NS), (1, 10, NS), (1, 3, 300_000_000), (1, 7, 1_500_000_000)],
+    "sw": [(2, 100, 60 * NS), (2, 5, 2 * NS), (2, 3, 1_500_000_000), (2, 4, 700_000_000), (2, 2, 300_000_000)],
+    "fw": [(3, 100, 60 * NS), (3, 5, 2 * NS), (3, 3, 1_500_000_000), (3, 4, 700_000_000), (3, 2, 7 * NS)],
+}
+CONFIG_SETS["mixed"] = CONFIG_SETS["tb"] + CONFIG_SETS["sw"] + CONFIG_SETS["fw"]
+
+
+def random_trace(seed, m, nkeys, configs, fastforward=False, big_n=False, one_cfg_per_key=True):
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, nkeys, m).astype(np.uint64)
+    gaps = rng.choice([0, 1, 1000, 250_000, 50_000_000, 700_000_000, 3 * NS], m,
+                      p=[0.05, 0.05, 0.4, 0.2, 0.2, 0.08, 0.02])
+    ts = T0 + np.cumsum(gaps).astype(np.int64)
+    n = rng.choice([1, 1, 1, 2, 3, 7, 50], m).astype(np.int64)
+    if big_n:
+        n[rng.random(m) < 0.02] = (1 << 62)
+        n[rng.random(m) < 0.01] = 0
+    if one_cfg_per_key:
+        cfg = (keys % len(configs)).astype(np.uint32)
+    else:
+        cfg = rng.integers(0, len(configs), m).astype(np.uint32)
+    sms = None
+    if fastforward:
+        sms = (ts // 1_000_000) + np.cumsum(rng.choice([0, 0, 0, 1500], m)).astype(np.int64)
+    return keys, ts, n, cfg, sms
