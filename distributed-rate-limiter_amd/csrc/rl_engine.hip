@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -100,20 +101,6 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     }
 }
 
-// segment heads: one entry per distinct slot (unordered list)
-__global__ __launch_bounds__(256) void k_heads(const uint32_t* __restrict__ sk, uint32_t m,
-                                               uint32_t invalid_key, uint32_t* __restrict__ seg_start,
-                                               uint32_t* nseg) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        uint32_t k = sk[i];
-        bool head = k != invalid_key && (i == 0 || sk[i - 1] != k);
-        if (head) {
-            uint32_t u = atomicAdd(nseg, 1u);
-            seg_start[u] = i;
-        }
-    }
-}
-
 // Reset: DEL of the key(s) AllowN would touch at ts (tokenbucket.go:136-144,
 // slidingwindow.go:125-139, fixedwindow.go:118-128)
 __global__ void k_reset(uint64_t key, int64_t ts, const CfgDev* cfgs, uint32_t cfg, TbEntry* tb,
@@ -149,8 +136,9 @@ namespace {
 constexpr int NSTAGES = 4;
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
-constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // segment count
-constexpr uint32_t CTRL_WORDS = CTRL_NSEG + 4;
+constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2,3] queue heads
+constexpr uint32_t CTRL_DBG = CTRL_NSEG + 4;   // [0] coop rounds [1] coop chunks
+constexpr uint32_t CTRL_WORDS = CTRL_DBG + 4;
 
 uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1;
@@ -185,7 +173,10 @@ struct rl_engine {
     uint32_t max_batch = 0;
     uint32_t max_tiles = 0;
     uint32_t *d_sk0 = nullptr, *d_sk1 = nullptr, *d_sv0 = nullptr, *d_sv1 = nullptr;
-    uint32_t* d_seg = nullptr;
+    SegRec* d_heavy = nullptr;
+    SegRec* d_light = nullptr;
+    int replay_grid = 2048;
+    uint32_t heavy_min = 32;   // segments this long replay cooperatively
     uint32_t* d_zero = nullptr;  // ctrl words + look-back status (memset per batch)
     size_t zero_bytes = 0;
     uint32_t* d_ctrl = nullptr;
@@ -227,7 +218,8 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_tb);
     (void)hipFree(e->d_win);
     (void)hipFree(e->d_sk0); (void)hipFree(e->d_sk1); (void)hipFree(e->d_sv0); (void)hipFree(e->d_sv1);
-    (void)hipFree(e->d_seg);
+    (void)hipFree(e->d_heavy);
+    (void)hipFree(e->d_light);
     (void)hipFree(e->d_zero);
     (void)hipFree(e->d_eflags);
     (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
@@ -267,7 +259,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_sk1, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_sv0, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_sv1, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_seg, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_heavy, sizeof(SegRec) * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_light, sizeof(SegRec) * M) == hipSuccess;
     e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
     ok &= hipMalloc(&e->d_zero, e->zero_bytes) == hipSuccess;
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
@@ -288,6 +281,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     k_init_win<<<2048, 256, 0, e->stream>>>(e->d_win, e->win_cap);
     if (hipMemsetAsync(e->d_eflags, 0, 4, e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
+    if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
+    if (const char* v = getenv("RL_REPLAY_GRID")) e->replay_grid = atoi(v);
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
     *out = e;
@@ -373,12 +368,14 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     }
     if (e->timing) (void)hipEventRecord(ev[2], s);
     // sorted keys/values are now in kin/vin
-    uint32_t* nseg = e->d_ctrl + CTRL_NSEG;
-    int grid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
-    k_heads<<<grid, 256, 0, s>>>(kin, m, e->invalid_key, e->d_seg, nseg);
+    uint32_t* segctr = e->d_ctrl + CTRL_NSEG;
+    int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
+    k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->heavy_min, e->d_heavy, segctr, e->d_light,
+                                      segctr + 1);
     if (e->timing) (void)hipEventRecord(ev[3], s);
-    k_replay_serial<<<grid, 256, 0, s>>>(kin, vin, m, e->d_seg, nseg, e->win_base, e->d_tb, e->d_win,
-                                         e->d_cfg, e->profile, a, e->d_eflags);
+    k_replay<<<e->replay_grid, COOP, 0, s>>>(kin, vin, e->d_heavy, segctr, e->d_light, segctr + 1, segctr + 2,
+                                            e->win_base, e->d_tb, e->d_win, e->d_cfg, e->profile, a,
+                                            e->d_eflags, e->d_ctrl + CTRL_DBG);
     if (e->timing) {
         (void)hipEventRecord(ev[4], s);
         e->ev_pending.push_back(ev);
@@ -470,6 +467,14 @@ extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t 
 
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     if (!e || !out) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    uint32_t c[8] = {0};
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(c, e->d_ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
+    e->stats.last_heavy = c[0];
+    e->stats.last_segments = (uint64_t)c[0] + c[1];
+    e->stats.last_coop_rounds = c[4];
+    e->stats.last_coop_chunks = c[5];
     *out = e->stats;
     return RL_OK;
 }

@@ -52,15 +52,35 @@ __device__ inline uint32_t seg_end(const uint32_t* sk, uint32_t m, uint32_t j0, 
     return lo + 1;
 }
 
+// one request's inputs, loaded one step ahead of use (the loads of step j+1
+// are in flight while step j computes: the segment walk is a dependent chain
+// of gathers otherwise)
+struct Req {
+    uint32_t i;
+    uint32_t c;
+    int64_t t, n, sms;
+};
+
+__device__ inline Req load_req(const ReqArgs& a, const uint32_t* sv, uint32_t j) {
+    Req r;
+    r.i = sv[j];
+    r.t = a.ts[r.i];
+    r.n = a.n[r.i];
+    r.c = a.cfg[r.i];
+    r.sms = a.sms ? a.sms[r.i] : floor_div(r.t, 1000000LL);
+    return r;
+}
+
 __device__ inline void replay_tb_serial(TbEntry* e, const uint32_t* sv, uint32_t j0, uint32_t j1,
                                         const CfgDev* cfgs, int32_t profile, const ReqArgs& a) {
     TbState st{e->tok, e->last, e->when};
+    Req cur = load_req(a, sv, j0);
     for (uint32_t j = j0; j < j1; j++) {
-        uint32_t i = sv[j];
-        int64_t t = a.ts[i];
-        const CfgDev& c = cfgs[a.cfg[i]];
-        Out o = tb_step(st, t, a.n[i], req_server_ms(a, i, t), c, profile);
-        write_out(a, i, o);
+        Req nxt = cur;
+        if (j + 1 < j1) nxt = load_req(a, sv, j + 1);
+        Out o = tb_step(st, cur.t, cur.n, cur.sms, cfgs[cur.c], profile);
+        write_out(a, cur.i, o);
+        cur = nxt;
     }
     e->tok = st.tok;
     e->last = st.last;
@@ -74,33 +94,320 @@ __device__ inline void replay_win_serial(WinEntry* e, const uint32_t* sv, uint32
     w.s[0] = e->s[0];
     w.s[1] = e->s[1];
     uint32_t ef = 0;
+    Req cur = load_req(a, sv, j0);
     for (uint32_t j = j0; j < j1; j++) {
-        uint32_t i = sv[j];
-        int64_t t = a.ts[i];
-        const CfgDev& c = cfgs[a.cfg[i]];
-        int64_t s_ms = req_server_ms(a, i, t);
-        Out o = (c.alg == ALG_SLIDING_WINDOW) ? sw_step(w, t, a.n[i], s_ms, c, profile, ef)
-                                              : fw_step(w, t, a.n[i], s_ms, c, profile, ef);
-        write_out(a, i, o);
+        Req nxt = cur;
+        if (j + 1 < j1) nxt = load_req(a, sv, j + 1);
+        const CfgDev& c = cfgs[cur.c];
+        Out o = (c.alg == ALG_SLIDING_WINDOW) ? sw_step(w, cur.t, cur.n, cur.sms, c, profile, ef)
+                                              : fw_step(w, cur.t, cur.n, cur.sms, c, profile, ef);
+        write_out(a, cur.i, o);
+        cur = nxt;
     }
     e->s[0] = w.s[0];
     e->s[1] = w.s[1];
     if (ef) atomicOr(eflags, ef);
 }
 
-// one thread per segment (grid-stride over the unordered segment list)
-__global__ __launch_bounds__(256) void k_replay_serial(
-    const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, uint32_t m,
-    const uint32_t* __restrict__ seg_start, const uint32_t* __restrict__ nseg_p, uint32_t win_base,
-    TbEntry* tb, WinEntry* win, const CfgDev* __restrict__ cfgs, int32_t profile, ReqArgs a,
-    uint32_t* eflags) {
-    const uint32_t nseg = *nseg_p;
-    for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < nseg; u += gridDim.x * blockDim.x) {
-        uint32_t j0 = seg_start[u];
-        uint32_t k0 = sk[j0];
-        uint32_t j1 = seg_end(sk, m, j0, k0);
-        if (k0 < win_base) replay_tb_serial(&tb[k0], sv, j0, j1, cfgs, profile, a);
-        else replay_win_serial(&win[k0 - win_base], sv, j0, j1, cfgs, profile, a, eflags);
+// ---------------------------------------------------------------------------
+// Block-cooperative token-bucket replay for heavy (Zipf hot-key) segments.
+//
+// The carried state of a token-bucket key is the *stored* tokens value, which
+// Lua's tostring quantizes: in Redis 7 to 14 significant decimal digits, i.e.
+// an integer D in [1e13, 1e14) and a decade E (value = D * 10^(E-13)); with
+// miniredis to the exact double, i.e. an integer mantissa D and binary
+// exponent E.  Between events a step's effect on D is the state-independent
+// increment r_j = round(add_j * 10^(13-E)) (resp. add_j * 2^-E), because D is
+// an integer and only the rounding of the fractional part of add_j matters.
+//
+// Guess-and-verify, one round per pass over the not-yet-committed lanes:
+//   1. each lane computes its nominal r_j (state-independent),
+//   2. block exclusive scan: guessed predecessor state Dg_j = D + sum r_<j,
+//   3. each lane runs the reference step EXACTLY (tb_step's arithmetic) from
+//      the guess and checks its exact result equals (Dg_j + r_j, E),
+//   4. the first lane s that does not (a near-tie rounding flip, a decade
+//      change, an allow, a clamp at capacity, an expired key) had a correct
+//      guess -- every lane before it was verified -- so lanes <= s are
+//      committed and s's exact result is the new base.
+// The result is identical to serial replay by construction; the common case
+// (denied requests accumulating refill) commits 256 steps per round.
+// ---------------------------------------------------------------------------
+constexpr int COOP = 256;
+constexpr int COOP_WAVES = COOP / 64;
+
+struct TbQ {
+    int64_t D;
+    int32_t E;
+};
+
+__device__ inline TbQ tb_quant(double x, int32_t profile) {
+    if (x == 0.0 || !(x - x == 0.0)) return TbQ{0, 0};
+    if (profile == PROFILE_REDIS7) {
+        double ax = x < 0 ? -x : x;
+        int64_t D;
+        int E;
+        if (!rlq::dec14_fast(ax, D, E)) rlq::dec14_slow(ax, D, E);
+        return TbQ{x < 0 ? -D : D, E};
+    }
+    int e;
+    double m = frexp(x, &e);
+    return TbQ{(int64_t)ldexp(m, 53), e - 53};
+}
+
+__device__ inline double tb_value(int64_t D, int32_t E, int32_t profile) {
+    if (D == 0) return 0.0;
+    if (profile == PROFILE_REDIS7) {
+        double v = rlq::dec14_value(D < 0 ? -D : D, E);
+        return D < 0 ? -v : v;
+    }
+    return ldexp((double)D, E);
+}
+
+// 1 / (unit of D) for decade/exponent E (only used for the nominal guess)
+__device__ inline double tb_scale(int32_t E, int32_t profile) {
+    if (profile != PROFILE_REDIS7) return ldexp(1.0, -E);
+    int k = 13 - E;
+    int ak = k < 0 ? -k : k;
+    double s = 1.0;
+    while (ak > 22) { s *= 1e22; ak -= 22; }
+    s *= rlq::pow10_exact(ak);
+    return k >= 0 ? s : 1.0 / s;
+}
+
+__device__ inline int64_t block_excl_scan_i64(int64_t v, int64_t* tmp) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        int64_t t = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) tmp[wave] = inc;
+    __syncthreads();
+    int64_t pre = 0;
+    for (int w = 0; w < wave; w++) pre += tmp[w];
+    __syncthreads();
+    return pre + inc - v;
+}
+
+// smallest thread index whose `flag` is set (COOP if none)
+__device__ inline uint32_t block_first_set(bool flag, uint32_t* tmp) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t mask = __ballot(flag);
+    if (lane == 0) tmp[wave] = mask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)mask) - 1) : COOP;
+    __syncthreads();
+    uint32_t r = COOP;
+    for (int w = 0; w < COOP_WAVES; w++) r = tmp[w] < r ? tmp[w] : r;
+    __syncthreads();
+    return r;
+}
+
+struct CoopShared {
+    double L[COOP];     // stored last_refill after each lane's step
+    int64_t W[COOP];    // key expiry after each lane's step
+    int64_t scan_tmp[COOP_WAVES];
+    uint32_t min_tmp[COOP_WAVES];
+    int64_t baseD;
+    int32_t baseE;
+    double carryL;
+    int64_t carryW;
+};
+
+__device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t* sv, uint32_t j0,
+                                      uint32_t j1, const CfgDev* cfgs, int32_t profile, const ReqArgs& a,
+                                      uint32_t* dbg) {
+    const uint32_t tid = threadIdx.x;
+    uint32_t nrounds = 0, nchunks = 0;
+    if (tid == 0) {
+        TbQ q = tb_quant(e->tok, profile);
+        sh.baseD = q.D;
+        sh.baseE = q.E;
+        sh.carryL = e->last;
+        sh.carryW = e->when;
+    }
+    __syncthreads();
+    for (uint32_t base = j0; base < j1; base += COOP) {
+        const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
+        const bool act = tid < cnt;
+        uint32_t i = 0;
+        int64_t t = 0, nn = 1, sms = 0;
+        const CfgDev* c = &cfgs[0];
+        if (act) {
+            i = sv[base + tid];
+            t = a.ts[i];
+            nn = a.n[i];
+            c = &cfgs[a.cfg[i]];
+            sms = req_server_ms(a, i, t);
+        }
+        const double now = (double)t / 1e9;
+        const double Lq = lua_tostring_roundtrip(now, profile);
+        const int64_t wafter = expire_when(c->ttl_tb, sms);
+        const int64_t reset_at = tb_reset_at(now, *c);
+        nchunks++;
+        sh.L[tid] = Lq;
+        sh.W[tid] = wafter;
+        __syncthreads();
+        const double prevL = tid ? sh.L[tid - 1] : sh.carryL;
+        const int64_t prevW = tid ? sh.W[tid - 1] : sh.carryW;
+        const bool alive = key_alive(prevW, sms, profile);
+        const double last = alive ? prevL : now;
+        const double add = (now - last) * c->rate;     // elapsed * refill_rate
+        const double cap = c->limit_d, nd = (double)nn;
+        uint32_t first = 0;
+        int32_t scaleE = INT32_MIN;
+        double scale = 0.0;
+        while (first < cnt) {                           // block-uniform
+            const int64_t D = sh.baseD;
+            const int32_t E = sh.baseE;
+            const bool mine = act && tid >= first;
+            nrounds++;
+            if (E != scaleE) { scale = tb_scale(E, profile); scaleE = E; }
+            int64_t r = 0;
+            bool force = !alive;
+            if (mine) {
+                double v = add * scale;
+                if (!(v < 1e15 && v > -1e15)) force = true;
+                else r = (int64_t)rint(v);
+            }
+            const int64_t Dg = D + block_excl_scan_i64(mine ? r : 0, sh.scan_tmp);
+            bool ok = false;
+            Out o;
+            TbQ q{0, 0};
+            if (mine) {
+                // tokenBucketScript from the guessed stored state (tokenbucket.go:32-51)
+                double T = alive ? tb_value(Dg, E, profile) : cap;
+                double sum = T + add;
+                double tokens = (sum < cap) ? sum : cap;
+                bool allowed = false;
+                if (tokens >= nd) { tokens = tokens - nd; allowed = true; }
+                q = tb_quant(tokens, profile);
+                int64_t rem = go_f2i(floor(tokens));
+                o.tokens = tokens;
+                o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
+                o.remaining = rem;
+                o.reset_at = reset_at;
+                o.retry = 0;
+                if (!allowed) {
+                    int64_t need = wsub(nn, rem);
+                    // tokensNeeded / refillRate (tokenbucket.go:124-126); 1/rate precomputed
+                    double w = need == 1 ? c->inv_rate : (double)need / c->rate;
+                    int64_t d = go_f2i(w * 1e9);
+                    o.retry = d < 0 ? 0 : d;
+                }
+                ok = !force && q.E == E && q.D == Dg + r;
+            }
+            uint32_t s = block_first_set(mine && !ok, sh.min_tmp);
+            if (s >= cnt) s = cnt - 1;
+            if (mine && tid <= s) write_out(a, i, o);
+            if (tid == s) {
+                sh.baseD = q.D;
+                sh.baseE = q.E;
+            }
+            __syncthreads();
+            first = s + 1;
+        }
+        if (tid == cnt - 1) {
+            sh.carryL = Lq;
+            sh.carryW = wafter;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        e->tok = tb_value(sh.baseD, sh.baseE, profile);
+        e->last = sh.carryL;
+        e->when = sh.carryW;
+        if (dbg) { atomicAdd(&dbg[0], nrounds); atomicAdd(&dbg[1], nchunks); }
+    }
+}
+
+struct SegRec {
+    uint32_t j0;
+    uint32_t len;
+};
+
+// segment heads -> (start, length), split into heavy (cooperative) and light
+// (one thread each) work lists.  One tile of SEG_TILE sorted positions per
+// block; list slots are reserved with ONE global atomic per list per block
+// (a single contended word sustains only ~88 atomics/us on MI355X).
+constexpr int SEG_ITEMS = 16;
+constexpr int SEG_TILE = 256 * SEG_ITEMS;
+
+__global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ sk, uint32_t m,
+                                                  uint32_t invalid_key, uint32_t heavy_min, SegRec* heavy,
+                                                  uint32_t* nheavy, SegRec* light, uint32_t* nlight) {
+    __shared__ uint32_t s_cnt[2], s_base[2];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t tile = blockIdx.x; tile * SEG_TILE < m; tile += gridDim.x) {
+        if (tid < 2) s_cnt[tid] = 0;
+        __syncthreads();
+        SegRec rec[SEG_ITEMS];
+        uint32_t slot[SEG_ITEMS];
+#pragma unroll
+        for (int j = 0; j < SEG_ITEMS; j++) {
+            uint32_t i = tile * SEG_TILE + j * 256 + tid;
+            slot[j] = 0xffffffffu;
+            if (i >= m) continue;
+            uint32_t k = sk[i];
+            bool head = k != invalid_key && (i == 0 || sk[i - 1] != k);
+            if (!head) continue;
+            uint32_t len = seg_end(sk, m, i, k) - i;
+            rec[j] = SegRec{i, len};
+            uint32_t which = len >= heavy_min ? 0u : 1u;
+            slot[j] = (which << 31) | atomicAdd(&s_cnt[which], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) s_base[0] = s_cnt[0] ? atomicAdd(nheavy, s_cnt[0]) : 0u;
+        if (tid == 1) s_base[1] = s_cnt[1] ? atomicAdd(nlight, s_cnt[1]) : 0u;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < SEG_ITEMS; j++) {
+            if (slot[j] == 0xffffffffu) continue;
+            uint32_t which = slot[j] >> 31, off = slot[j] & 0x7fffffffu;
+            if (which == 0) heavy[s_base[0] + off] = rec[j];
+            else light[s_base[1] + off] = rec[j];
+        }
+        __syncthreads();
+    }
+}
+
+// Work-queue replay: blocks first drain the heavy list (one segment per block,
+// cooperative), then the light list (256 segments per grab, one per thread).
+__global__ __launch_bounds__(COOP) void k_replay(
+    const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, const SegRec* __restrict__ heavy,
+    const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
+    const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
+    const CfgDev* __restrict__ cfgs, int32_t profile, ReqArgs a, uint32_t* eflags, uint32_t* dbg) {
+    __shared__ CoopShared sh;
+    __shared__ uint32_t s_u;
+    const uint32_t nheavy = *nheavy_p, nlight = *nlight_p;
+    for (;;) {
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
+        __syncthreads();
+        const uint32_t u = s_u;
+        __syncthreads();
+        if (u >= nheavy) break;
+        const SegRec sg = heavy[u];
+        const uint32_t k0 = sk[sg.j0];
+        if (k0 < win_base) {
+            replay_tb_coop(sh, &tb[k0], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a, dbg);
+        } else if (threadIdx.x == 0) {
+            replay_win_serial(&win[k0 - win_base], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+        }
+        __syncthreads();
+    }
+    for (;;) {
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)COOP);
+        __syncthreads();
+        const uint32_t u0 = s_u;
+        __syncthreads();
+        if (u0 >= nlight) break;
+        const uint32_t u = u0 + threadIdx.x;
+        if (u < nlight) {
+            const SegRec sg = light[u];
+            const uint32_t k0 = sk[sg.j0];
+            if (k0 < win_base) replay_tb_serial(&tb[k0], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a);
+            else replay_win_serial(&win[k0 - win_base], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+        }
     }
 }
 

@@ -46,6 +46,7 @@ struct CfgDev {
     int64_t ttl_p;       // int64(W.Seconds()*2)  (slidingwindow.go:162)
     int64_t off_mod;     // (62135596800 s) mod W, for Truncate relative to year 1
     int64_t tb_full_ns;  // time.Duration(float64(L)/rate * 1e9) (tokenbucket.go:163-164)
+    double inv_rate;     // float64(1) / rate: tokensNeeded / refillRate for tokensNeeded == 1
 };
 
 // Go's int64(float64) on amd64 (CVTTSD2SQ): truncate; NaN / out of range -> MinInt64.
@@ -77,6 +78,7 @@ inline CfgDev make_cfg(int32_t alg, int64_t limit, int64_t window) {
     __int128 off = (__int128)62135596800LL * NS_PER_S;  // Go unixToInternal, in ns
     c.off_mod = (int64_t)(off % window);
     c.tb_full_ns = go_f2i((double)limit / c.rate * 1e9);  // tokenbucket.go:163-164
+    c.inv_rate = 1.0 / c.rate;
     return c;
 }
 
@@ -172,8 +174,9 @@ RL_HD inline Out tb_step(TbState& st, int64_t t, int64_t n, int64_t s_ms, const 
     o.reset_at = tb_reset_at(now, c);
     o.retry = 0;
     if (!allowed) {
-        double needed = (double)wsub(n, rem);
-        int64_t d = go_f2i(needed / c.rate * 1e9);
+        int64_t need = wsub(n, rem);
+        double w = need == 1 ? c.inv_rate : (double)need / c.rate;   // tokensNeeded / refillRate
+        int64_t d = go_f2i(w * 1e9);
         o.retry = d < 0 ? 0 : d;
     }
     return o;

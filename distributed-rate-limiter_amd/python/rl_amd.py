@@ -53,6 +53,8 @@ class rl_stats(C.Structure):
         ("decisions", C.c_uint64),
         ("last_segments", C.c_uint64),
         ("last_heavy", C.c_uint64),
+        ("last_coop_rounds", C.c_uint64),
+        ("last_coop_chunks", C.c_uint64),
         ("sort_bits", C.c_uint32),
         ("sort_passes", C.c_uint32),
     ]

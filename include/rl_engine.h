@@ -69,6 +69,8 @@ typedef struct rl_stats {
     uint64_t decisions;
     uint64_t last_segments;   /* distinct keys in the last batch */
     uint64_t last_heavy;      /* segments replayed cooperatively in the last batch */
+    uint64_t last_coop_rounds; /* guess-and-verify rounds of the last batch (all heavy segments) */
+    uint64_t last_coop_chunks; /* 256-request chunks of the last batch's heavy segments */
     uint32_t sort_bits;
     uint32_t sort_passes;
 } rl_stats;

@@ -40,7 +40,8 @@ def run_both(rl, profile, configs, batches, **kw):
     sim = oracle.OracleSim(profile)
     for a, L, W in configs:
         assert eng.register(a, L, W) == sim.add_config(a, L, W)
-    for i, (key, ts, n, cfg, sms) in enumerate(batches):
+    for i, b in enumerate(batches):
+        key, ts, n, cfg, sms = b if len(b) == 5 else (*b, None)
         res = eng.decide(key, ts, n, cfg, sms)
         ref = sim.decide(key, ts, n, cfg, sms)
         assert_same(res, ref, configs, cfg, what=f"batch {i}")
