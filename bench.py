@@ -199,6 +199,7 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_decision": bytes_per_dec},
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
+                          "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_chunks": int(st.last_coop_chunks)},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
                                                     (stage_ms / nbat).tolist())},

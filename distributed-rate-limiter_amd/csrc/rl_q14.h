@@ -29,11 +29,17 @@
 #include <math.h>
 #define RL_HD
 #endif
+// Fast paths are forced inline: an out-of-line call on AMDGPU sets up a stack
+// frame in scratch memory on every step.  The big-integer slow paths (rare:
+// |x| < 1e-9 or >= 1e35) stay out of line so their arrays never touch the
+// hot loop's registers.
+#define RL_INLINE RL_HD inline __attribute__((always_inline))
+#define RL_COLD RL_HD inline __attribute__((noinline))
 
 namespace rlq {
 
 // 10^k, k in [0,22]: every partial product is a power of ten <= 1e22, hence exact.
-RL_HD inline double pow10_exact(int k) {
+RL_INLINE double pow10_exact(int k) {
     double p = 1.0;
     if (k & 1) p *= 1e1;
     if (k & 2) p *= 1e2;
@@ -43,19 +49,19 @@ RL_HD inline double pow10_exact(int k) {
     return p;
 }
 
-RL_HD inline uint64_t dbits(double x) {
+RL_INLINE uint64_t dbits(double x) {
     union { double d; uint64_t u; } v; v.d = x; return v.u;
 }
-RL_HD inline double bitsd(uint64_t u) {
+RL_INLINE double bitsd(uint64_t u) {
     union { double d; uint64_t u; } v; v.u = u; return v.d;
 }
 
 // floor(e2 * log10(2)) for |e2| <= 2000
-RL_HD inline int floor_log10_pow2(int e2) { return (e2 * 78913) >> 18; }
+RL_INLINE int floor_log10_pow2(int e2) { return (e2 * 78913) >> 18; }
 
 // Round a * 10^k (a > 0, |k| <= 22, result < 2^47) to the nearest integer,
 // ties to even, exactly.
-RL_HD inline int64_t round_scaled(double a, int k) {
+RL_INLINE int64_t round_scaled(double a, int k) {
     double p, err;
     if (k >= 0) {
         double P = pow10_exact(k);
@@ -164,7 +170,7 @@ RL_HD inline uint64_t bn_divmod_small_q(Big& N, const Big& Q, int qbits) {
 }
 
 // exact round(a * 10^k) to nearest-even integer (result < 2^48); a = m * 2^e
-RL_HD inline int64_t round_scaled_big(uint64_t m, int e, int k) {
+RL_COLD int64_t round_scaled_big(uint64_t m, int e, int k) {
     Big N, Q;
     bn_set_u64(N, m);
     bn_set_u64(Q, 1);
@@ -201,7 +207,7 @@ RL_HD inline double round_to_double(uint64_t q, int b, bool sticky) {
 }
 
 // correctly rounded D * 10^j (D < 2^48, any j in [-400, 400]) as strtod would
-RL_HD inline double dec_to_double_big(int64_t D, int j) {
+RL_COLD double dec_to_double_big(int64_t D, int j) {
     Big X;
     bn_set_u64(X, (uint64_t)D);
     if (j >= 0) {
@@ -232,7 +238,7 @@ RL_HD inline double dec_to_double_big(int64_t D, int j) {
 
 // 14-significant-digit decimal of |x| (x finite, nonzero): |x| ~ D * 10^(E-13),
 // D in [1e13, 1e14).  Returns false if the slow path was needed.
-RL_HD inline bool dec14_fast(double a, int64_t& D, int& E) {
+RL_INLINE bool dec14_fast(double a, int64_t& D, int& E) {
     int e2 = (int)((dbits(a) >> 52) & 0x7ff) - 1023;
     if (e2 < -1022) return false;                // subnormal: slow path
     int E0 = floor_log10_pow2(e2);
@@ -246,7 +252,7 @@ RL_HD inline bool dec14_fast(double a, int64_t& D, int& E) {
     return true;
 }
 
-RL_HD inline void dec14_slow(double a, int64_t& D, int& E) {
+RL_COLD void dec14_slow(double a, int64_t& D, int& E) {
     uint64_t bits = dbits(a);
     int ex = (int)((bits >> 52) & 0x7ff);
     uint64_t m = bits & ((1ULL << 52) - 1);
@@ -263,7 +269,7 @@ RL_HD inline void dec14_slow(double a, int64_t& D, int& E) {
 }
 
 // strtod of D * 10^(E-13), D < 2^47
-RL_HD inline double dec14_value(int64_t D, int E) {
+RL_INLINE double dec14_value(int64_t D, int E) {
     int j = E - 13;
     if (j >= -22 && j <= 22) {
         double d = (double)D;                     // exact
@@ -273,7 +279,7 @@ RL_HD inline double dec14_value(int64_t D, int E) {
 }
 
 // tonumber(tostring(x)) in Redis 7's Lua 5.1
-RL_HD inline double q14(double x) {
+RL_INLINE double q14(double x) {
     if (x == 0.0 || !(x - x == 0.0)) return x;   // +-0, inf, nan round-trip unchanged
     double a = x < 0 ? -x : x;
     int64_t D;

@@ -174,32 +174,43 @@ __device__ inline double tb_scale(int32_t E, int32_t profile) {
     return k >= 0 ? s : 1.0 / s;
 }
 
-__device__ inline int64_t block_excl_scan_i64(int64_t v, int64_t* tmp) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int64_t inc = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        int64_t t = __shfl_up(inc, off, 64);
-        if (lane >= off) inc += t;
-    }
-    if (lane == 63) tmp[wave] = inc;
-    __syncthreads();
-    int64_t pre = 0;
-    for (int w = 0; w < wave; w++) pre += tmp[w];
-    __syncthreads();
-    return pre + inc - v;
+// Diagnostic build only (-DRL_STAMPS): per-phase shader-clock sums of the
+// cooperative replay, read back through the debug counters; never in the
+// product build (stamps serialize the phases they measure).
+#ifdef RL_STAMPS
+#define RL_STAMP(v) do { __builtin_amdgcn_sched_barrier(0); (v) = __builtin_amdgcn_s_memtime(); \
+                         __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define RL_STAMP(v) do { } while (0)
+#endif
+
+// Barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope
+// fence on gfx950 and waits for every outstanding global store (vmcnt(0));
+// the replay rounds scatter results to HBM between barriers and must not wait
+// for them.  LDS writes are complete once lgkmcnt reaches 0.
+__device__ inline void lds_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// smallest thread index whose `flag` is set (COOP if none)
-__device__ inline uint32_t block_first_set(bool flag, uint32_t* tmp) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint64_t mask = __ballot(flag);
-    if (lane == 0) tmp[wave] = mask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)mask) - 1) : COOP;
-    __syncthreads();
-    uint32_t r = COOP;
-    for (int w = 0; w < COOP_WAVES; w++) r = tmp[w] < r ? tmp[w] : r;
-    __syncthreads();
-    return r;
+// 64-bit wave64 inclusive scan with DPP row shifts and row broadcasts (GFX9
+// family): 6 steps of two v_mov_dpp + a 64-bit add, no LDS round trips.
+template <int CTRL, int ROW_MASK>
+__device__ inline int64_t dpp_add_step(int64_t inc) {
+    uint32_t lo = (uint32_t)inc, hi = (uint32_t)((uint64_t)inc >> 32);
+    // old = 0: lanes with no source (or outside ROW_MASK) contribute 0
+    uint32_t slo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, ROW_MASK, 0xf, false);
+    uint32_t shi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, ROW_MASK, 0xf, false);
+    return inc + (int64_t)(((uint64_t)shi << 32) | slo);
+}
+
+__device__ inline int64_t wave_incl_scan_i64(int64_t v) {
+    v = dpp_add_step<0x111, 0xf>(v);   // row_shr:1
+    v = dpp_add_step<0x112, 0xf>(v);   // row_shr:2
+    v = dpp_add_step<0x114, 0xf>(v);   // row_shr:4
+    v = dpp_add_step<0x118, 0xf>(v);   // row_shr:8
+    v = dpp_add_step<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+    v = dpp_add_step<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
+    return v;
 }
 
 struct CoopShared {
@@ -218,6 +229,8 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
                                       uint32_t* dbg) {
     const uint32_t tid = threadIdx.x;
     uint32_t nrounds = 0, nchunks = 0;
+    uint64_t cyc[5] = {0, 0, 0, 0, 0}, t0 = 0, t1 = 0;
+    (void)cyc; (void)t0; (void)t1;
     if (tid == 0) {
         TbQ q = tb_quant(e->tok, profile);
         sh.baseD = q.D;
@@ -229,6 +242,7 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
     for (uint32_t base = j0; base < j1; base += COOP) {
         const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
         const bool act = tid < cnt;
+        RL_STAMP(t0);
         uint32_t i = 0;
         int64_t t = 0, nn = 1, sms = 0;
         const CfgDev* c = &cfgs[0];
@@ -253,9 +267,14 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
         const double last = alive ? prevL : now;
         const double add = (now - last) * c->rate;     // elapsed * refill_rate
         const double cap = c->limit_d, nd = (double)nn;
+        RL_STAMP(t1);
+#ifdef RL_STAMPS
+        cyc[0] += t1 - t0;
+#endif
         uint32_t first = 0;
         int32_t scaleE = INT32_MIN;
         double scale = 0.0;
+        const uint32_t lane = tid & 63, wave = tid >> 6;
         while (first < cnt) {                           // block-uniform
             const int64_t D = sh.baseD;
             const int32_t E = sh.baseE;
@@ -269,7 +288,19 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
                 if (!(v < 1e15 && v > -1e15)) force = true;
                 else r = (int64_t)rint(v);
             }
-            const int64_t Dg = D + block_excl_scan_i64(mine ? r : 0, sh.scan_tmp);
+            // exclusive block scan of r: DPP within the wave, wave totals via LDS
+            RL_STAMP(t0);
+            const int64_t rin = mine ? r : 0;
+            const int64_t inc = wave_incl_scan_i64(rin);
+            if (lane == 63) sh.scan_tmp[wave] = inc;
+            lds_barrier();                                               // A
+            int64_t pre = 0;
+            for (uint32_t w = 0; w < wave; w++) pre += sh.scan_tmp[w];
+            const int64_t Dg = D + pre + inc - rin;
+            RL_STAMP(t1);
+#ifdef RL_STAMPS
+            cyc[1] += t1 - t0; t0 = t1;
+#endif
             bool ok = false;
             Out o;
             TbQ q{0, 0};
@@ -296,14 +327,31 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
                 }
                 ok = !force && q.E == E && q.D == Dg + r;
             }
-            uint32_t s = block_first_set(mine && !ok, sh.min_tmp);
+            RL_STAMP(t1);
+#ifdef RL_STAMPS
+            cyc[2] += t1 - t0; t0 = t1;
+#endif
+            // first lane whose exact result differs from its guess
+            const uint64_t bad = __ballot(mine && !ok);
+            if (lane == 0) sh.min_tmp[wave] = bad ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bad) - 1) : COOP;
+            lds_barrier();                                               // B
+            uint32_t s = COOP;
+            for (int w = 0; w < COOP_WAVES; w++) s = sh.min_tmp[w] < s ? sh.min_tmp[w] : s;
             if (s >= cnt) s = cnt - 1;
+            RL_STAMP(t1);
+#ifdef RL_STAMPS
+            cyc[3] += t1 - t0; t0 = t1;
+#endif
             if (mine && tid <= s) write_out(a, i, o);
             if (tid == s) {
                 sh.baseD = q.D;
                 sh.baseE = q.E;
             }
-            __syncthreads();
+            lds_barrier();                                               // C
+            RL_STAMP(t1);
+#ifdef RL_STAMPS
+            cyc[4] += t1 - t0;
+#endif
             first = s + 1;
         }
         if (tid == cnt - 1) {
@@ -317,6 +365,10 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
         e->last = sh.carryL;
         e->when = sh.carryW;
         if (dbg) { atomicAdd(&dbg[0], nrounds); atomicAdd(&dbg[1], nchunks); }
+#ifdef RL_STAMPS
+        // phase cycles of the LONGEST cooperative segment of the batch (max)
+        if (dbg) for (int k = 0; k < 5; k++) atomicMax((unsigned long long*)&dbg[8 + 2 * k], (unsigned long long)cyc[k]);
+#endif
     }
 }
 

@@ -14,7 +14,7 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "librl_amd.so")
+LIB_PATH = os.environ.get("RL_AMD_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "librl_amd.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -57,6 +57,7 @@ class rl_stats(C.Structure):
         ("last_coop_chunks", C.c_uint64),
         ("sort_bits", C.c_uint32),
         ("sort_passes", C.c_uint32),
+        ("stamp_cycles", C.c_uint64 * 5),
     ]
 
 
