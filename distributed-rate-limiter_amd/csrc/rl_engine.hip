@@ -373,7 +373,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->heavy_min, e->d_heavy, segctr, e->d_light,
                                       segctr + 1);
     if (e->timing) (void)hipEventRecord(ev[3], s);
-    k_replay<<<e->replay_grid, COOP, 0, s>>>(kin, vin, e->d_heavy, segctr, e->d_light, segctr + 1, segctr + 2,
+    k_replay<<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, vin, e->d_heavy, segctr, e->d_light, segctr + 1, segctr + 2,
                                             e->win_base, e->d_tb, e->d_win, e->d_cfg, e->profile, a,
                                             e->d_eflags, e->d_ctrl + CTRL_DBG);
     if (e->timing) {

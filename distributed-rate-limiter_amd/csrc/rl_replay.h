@@ -213,21 +213,41 @@ __device__ inline int64_t wave_incl_scan_i64(int64_t v) {
     return v;
 }
 
+// One chunk's requests as the loader wave hands them to the compute waves.
+struct ChunkSlot {
+    int64_t t, n, sms;
+    uint32_t i, c;
+};
+
 struct CoopShared {
-    double L[COOP];     // stored last_refill after each lane's step
-    int64_t W[COOP];    // key expiry after each lane's step
+    ChunkSlot ring[2][COOP];  // requests of chunk k (slot k&1), filled by the loader wave
+    double L[COOP];           // stored last_refill after each lane's step
+    int64_t W[COOP];          // key expiry after each lane's step
     int64_t scan_tmp[COOP_WAVES];
     uint32_t min_tmp[COOP_WAVES];
     int64_t baseD;
     int32_t baseE;
+    uint32_t need_full;       // committed lane must re-quantize its tokens
     double carryL;
     int64_t carryW;
+    double full_tokens;
 };
 
-__device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t* sv, uint32_t j0,
-                                      uint32_t j1, const CfgDev* cfgs, int32_t profile, const ReqArgs& a,
-                                      uint32_t* dbg) {
+// The replay block: COOP compute lanes (4 waves) + one loader wave.  The
+// loader is the only wave that issues the request gathers (sv -> ts, n, cfg,
+// server_ms), two chunks ahead, into an LDS ring.  On gfx9 loads and stores
+// share vmcnt, so a compute wave that both scattered results and waited on
+// its own prefetch would wait for its stores; here compute waves never wait
+// on global memory in the steady state.
+constexpr int REPLAY_BLOCK = COOP + 64;
+constexpr uint32_t NO_REQ = 0xffffffffu;
+
+__device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t* __restrict__ sv, uint32_t j0,
+                                      uint32_t j1, const CfgDev* __restrict__ cfgs, int32_t profile,
+                                      const ReqArgs& a, uint32_t* dbg) {
     const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63, wave = tid >> 6;
+    const bool loader = wave == COOP_WAVES;
     uint32_t nrounds = 0, nchunks = 0;
     uint64_t cyc[5] = {0, 0, 0, 0, 0}, t0 = 0, t1 = 0;
     (void)cyc; (void)t0; (void)t1;
@@ -238,49 +258,93 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
         sh.carryL = e->last;
         sh.carryW = e->when;
     }
-    __syncthreads();
-    for (uint32_t base = j0; base < j1; base += COOP) {
-        const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
-        const bool act = tid < cnt;
-        RL_STAMP(t0);
-        uint32_t i = 0;
-        int64_t t = 0, nn = 1, sms = 0;
-        const CfgDev* c = &cfgs[0];
-        if (act) {
-            i = sv[base + tid];
-            t = a.ts[i];
-            nn = a.n[i];
-            c = &cfgs[a.cfg[i]];
-            sms = req_server_ms(a, i, t);
+    const uint32_t c0 = a.cfg[sv[j0]];
+    const CfgDev cf0 = cfgs[c0];
+    // loader state: request indices of the next chunk (4 per loader lane)
+    uint32_t idx[4];
+    ChunkSlot fld[4];
+    auto ld_idx = [&](uint32_t base) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t j = base + lane + 64 * q;
+            idx[q] = (base < j1 && j < j1) ? sv[j] : NO_REQ;
         }
-        const double now = (double)t / 1e9;
-        const double Lq = lua_tostring_roundtrip(now, profile);
-        const int64_t wafter = expire_when(c->ttl_tb, sms);
-        const int64_t reset_at = tb_reset_at(now, *c);
+    };
+    auto ld_fields = [&]() {
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t i = idx[q];
+            ChunkSlot f{0, 1, 0, i, c0};
+            if (i != NO_REQ) {
+                f.t = a.ts[i];
+                f.n = a.n[i];
+                f.c = a.cfg[i];
+                f.sms = a.sms ? a.sms[i] : floor_div(f.t, 1000000LL);
+            }
+            fld[q] = f;
+        }
+    };
+    auto st_fields = [&](int slot) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) sh.ring[slot][lane + 64 * q] = fld[q];
+    };
+    if (loader) {            // prologue: chunk 0 into slot 0, chunk 1's indices in flight
+        ld_idx(j0);
+        ld_fields();
+        st_fields(0);
+        ld_idx(j0 + COOP);
+    }
+    __syncthreads();
+    uint32_t k = 0;
+    for (uint32_t base = j0; base < j1; base += COOP, k++) {
+        const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
+        const bool act = !loader && tid < cnt;
+        RL_STAMP(t0);
+        if (loader) {        // chunk k+1's fields, chunk k+2's indices: land during this chunk
+            ld_fields();
+            ld_idx(base + 2 * COOP);
+        }
+        ChunkSlot rq = loader ? ChunkSlot{0, 1, 0, NO_REQ, c0} : sh.ring[k & 1][tid];
+        const uint32_t i = rq.i;
+        const int64_t t = rq.t, nn = rq.n, sms = rq.sms;
+        const CfgDev cf = (rq.c == c0) ? cf0 : cfgs[rq.c];
         nchunks++;
-        sh.L[tid] = Lq;
-        sh.W[tid] = wafter;
-        __syncthreads();
-        const double prevL = tid ? sh.L[tid - 1] : sh.carryL;
-        const int64_t prevW = tid ? sh.W[tid - 1] : sh.carryW;
+        const double now = (double)t / 1e9;
+        const double Lq = act ? lua_tostring_roundtrip(now, profile) : 0.0;
+        const int64_t wafter = expire_when(cf.ttl_tb, sms);
+        const int64_t reset_at = tb_reset_at(now, cf);
+        if (!loader) {
+            sh.L[tid] = Lq;
+            sh.W[tid] = wafter;
+        }
+        lds_barrier();
+        const uint32_t pv = (tid > 0 && tid < (uint32_t)COOP) ? tid - 1 : 0;
+        const double prevL = tid ? sh.L[pv] : sh.carryL;
+        const int64_t prevW = tid ? sh.W[pv] : sh.carryW;
         const bool alive = key_alive(prevW, sms, profile);
         const double last = alive ? prevL : now;
-        const double add = (now - last) * c->rate;     // elapsed * refill_rate
-        const double cap = c->limit_d, nd = (double)nn;
+        const double add = (now - last) * cf.rate;     // elapsed * refill_rate
+        const double cap = cf.limit_d, nd = (double)nn, rate = cf.rate, inv_rate = cf.inv_rate;
         RL_STAMP(t1);
 #ifdef RL_STAMPS
         cyc[0] += t1 - t0;
 #endif
         uint32_t first = 0;
         int32_t scaleE = INT32_MIN;
-        double scale = 0.0;
-        const uint32_t lane = tid & 63, wave = tid >> 6;
+        double scale = 0.0, P = 1.0, R = 1.0;
+        bool fastdec = false;
         while (first < cnt) {                           // block-uniform
             const int64_t D = sh.baseD;
             const int32_t E = sh.baseE;
             const bool mine = act && tid >= first;
             nrounds++;
-            if (E != scaleE) { scale = tb_scale(E, profile); scaleE = E; }
+            if (E != scaleE) {
+                scaleE = E;
+                scale = tb_scale(E, profile);
+                // Redis profile, decade with an exact power of ten: short chain
+                fastdec = profile == PROFILE_REDIS7 && (13 - E) >= 1 && (13 - E) <= 22;
+                if (fastdec) { P = rlq::pow10_exact(13 - E); R = 1.0 / P; }
+            }
             int64_t r = 0;
             bool force = !alive;
             if (mine) {
@@ -292,26 +356,45 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
             RL_STAMP(t0);
             const int64_t rin = mine ? r : 0;
             const int64_t inc = wave_incl_scan_i64(rin);
-            if (lane == 63) sh.scan_tmp[wave] = inc;
+            if (lane == 63 && !loader) sh.scan_tmp[wave] = inc;
             lds_barrier();                                               // A
             int64_t pre = 0;
-            for (uint32_t w = 0; w < wave; w++) pre += sh.scan_tmp[w];
+            for (uint32_t w = 0; w < wave && w < (uint32_t)COOP_WAVES; w++) pre += sh.scan_tmp[w];
             const int64_t Dg = D + pre + inc - rin;
             RL_STAMP(t1);
 #ifdef RL_STAMPS
             cyc[1] += t1 - t0; t0 = t1;
 #endif
-            bool ok = false;
+            bool ok = false, full = false;
             Out o;
             TbQ q{0, 0};
+            double tokens = 0.0;
             if (mine) {
                 // tokenBucketScript from the guessed stored state (tokenbucket.go:32-51)
-                double T = alive ? tb_value(Dg, E, profile) : cap;
+                double T;
+                if (!alive) T = cap;
+                else if (fastdec && Dg > 0) T = rlq::div_pow10((double)Dg, P, R);   // == strtod(D e(E-13))
+                else T = tb_value(Dg, E, profile);
                 double sum = T + add;
-                double tokens = (sum < cap) ? sum : cap;
+                tokens = (sum < cap) ? sum : cap;
                 bool allowed = false;
                 if (tokens >= nd) { tokens = tokens - nd; allowed = true; }
-                q = tb_quant(tokens, profile);
+                // tonumber(tostring(tokens)) as (digits, decade), and is it the guess?
+                const int64_t Dexp = Dg + r;
+                if (fastdec && tokens > 0.0 && tokens * P < 1.4e14) {
+                    const int64_t Dact = rlq::round_scaled_P(tokens, P);
+                    const bool inrange = Dact >= 10000000000000LL && Dact < 100000000000000LL;
+                    ok = !force && inrange && Dact == Dexp;
+                    full = !inrange;
+                    q = TbQ{Dact, E};
+                } else if (profile != PROFILE_REDIS7) {
+                    int64_t ad = Dexp < 0 ? -Dexp : Dexp;
+                    ok = !force && ad >= (1LL << 52) && ad < (1LL << 53) && tokens == ldexp((double)Dexp, E);
+                    full = !ok;
+                    q = TbQ{Dexp, E};
+                } else {
+                    full = true;    // off the fast decades: quantize in full if this lane commits
+                }
                 int64_t rem = go_f2i(floor(tokens));
                 o.tokens = tokens;
                 o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
@@ -321,11 +404,10 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
                 if (!allowed) {
                     int64_t need = wsub(nn, rem);
                     // tokensNeeded / refillRate (tokenbucket.go:124-126); 1/rate precomputed
-                    double w = need == 1 ? c->inv_rate : (double)need / c->rate;
+                    double w = need == 1 ? inv_rate : (double)need / rate;
                     int64_t d = go_f2i(w * 1e9);
                     o.retry = d < 0 ? 0 : d;
                 }
-                ok = !force && q.E == E && q.D == Dg + r;
             }
             RL_STAMP(t1);
 #ifdef RL_STAMPS
@@ -333,7 +415,8 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
 #endif
             // first lane whose exact result differs from its guess
             const uint64_t bad = __ballot(mine && !ok);
-            if (lane == 0) sh.min_tmp[wave] = bad ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bad) - 1) : COOP;
+            if (lane == 0 && !loader)
+                sh.min_tmp[wave] = bad ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bad) - 1) : COOP;
             lds_barrier();                                               // B
             uint32_t s = COOP;
             for (int w = 0; w < COOP_WAVES; w++) s = sh.min_tmp[w] < s ? sh.min_tmp[w] : s;
@@ -344,6 +427,7 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
 #endif
             if (mine && tid <= s) write_out(a, i, o);
             if (tid == s) {
+                if (full) q = tb_quant(tokens, profile);   // decade change, allow, zero, slow path
                 sh.baseD = q.D;
                 sh.baseE = q.E;
             }
@@ -358,7 +442,8 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
             sh.carryL = Lq;
             sh.carryW = wafter;
         }
-        __syncthreads();
+        if (loader) st_fields((k + 1) & 1);   // chunk k+1 (loaded during this chunk's rounds)
+        lds_barrier();
     }
     if (tid == 0) {
         e->tok = tb_value(sh.baseD, sh.baseE, profile);
@@ -424,7 +509,7 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
 
 // Work-queue replay: blocks first drain the heavy list (one segment per block,
 // cooperative), then the light list (256 segments per grab, one per thread).
-__global__ __launch_bounds__(COOP) void k_replay(
+__global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, const SegRec* __restrict__ heavy,
     const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
     const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
@@ -448,7 +533,7 @@ __global__ __launch_bounds__(COOP) void k_replay(
         __syncthreads();
     }
     for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)COOP);
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)REPLAY_BLOCK);
         __syncthreads();
         const uint32_t u0 = s_u;
         __syncthreads();

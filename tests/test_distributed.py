@@ -1,0 +1,106 @@
+"""Multi-rank sharding (world_size 2, gloo, CPU): routing every rank's
+requests to the key's owner with all-to-all, deciding there, and returning
+results in the original order gives exactly the decisions of ONE shared
+limiter over the union of the ranks' requests (as the reference's N app
+servers sharing one Redis).  The per-owner decider here is the CPU oracle
+(test infrastructure); on the GPU box it is the HIP engine."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tracegen import CONFIG_SETS, T0
+
+CONFIGS = CONFIG_SETS["mixed"]
+
+
+def rank_batches(rank, nbatch=3, m=4000):
+    rng = np.random.default_rng(100 + rank)
+    t = T0
+    out = []
+    for _ in range(nbatch):
+        key = rng.integers(0, 300, m).astype(np.uint64)
+        ts = t + np.cumsum(rng.integers(0, 400_000, m)).astype(np.int64)
+        t = int(ts[-1]) + 1
+        n = rng.choice([1, 1, 2, 5], m).astype(np.int64)
+        cfg = (key % len(CONFIGS)).astype(np.uint32)
+        out.append((key, ts, n, cfg))
+    return out
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "distributed-rate-limiter_amd", "python"),
+                    os.path.join(root, "tests")]
+    import torch.distributed as dist
+
+    import oracle
+    import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sim = oracle.OracleSim(0)
+        for a, L, W in CONFIGS:
+            sim.add_config(a, L, W)
+
+        def decide(key, ts, n, cfg):
+            d, r, rt, rs, _ = sim.decide(key, ts, n, cfg)
+            return d, r, rt, rs
+
+        ref = oracle.OracleSim(0)
+        for a, L, W in CONFIGS:
+            ref.add_config(a, L, W)
+        all_batches = [rank_batches(r) for r in range(world)]
+        ok = True
+        for b in range(3):
+            key, ts, n, cfg = all_batches[rank][b]
+            got = shard.route_and_decide(key, ts, n, cfg, decide)
+            # expectation: one shared limiter over the union, ordered (ts, rank, pos)
+            parts = [all_batches[r][b] for r in range(world)]
+            U = [np.concatenate([p[f] for p in parts]) for f in range(4)]
+            src = np.concatenate([np.full(p[0].size, r) for r, p in enumerate(parts)])
+            pos = np.concatenate([np.arange(p[0].size) for p in parts])
+            o = np.lexsort((pos, src, U[1]))
+            d, rm, rt, rs, _ = ref.decide(U[0][o], U[1][o], U[2][o], U[3][o])
+            mine = src[o] == rank
+            exp_pos = pos[o][mine]
+            exp = [x[mine] for x in (d, rm, rt, rs)]
+            inv = np.empty_like(exp_pos)
+            inv[exp_pos] = np.arange(exp_pos.size)
+            for g, e in zip(got, exp):
+                ok &= bool(np.array_equal(np.asarray(g, np.int64), np.asarray(e, np.int64)[inv]))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_routed_sharding_matches_single_shared_limiter():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}
+
+
+def test_owner_partition_is_balanced():
+    import shard
+    key = np.arange(1_000_000, dtype=np.uint64)
+    for world in (2, 4, 8):
+        c = np.bincount(shard.owner_of(key, world), minlength=world)
+        assert c.min() > 0.97 * key.size / world
