@@ -174,6 +174,12 @@ struct rl_engine {
     uint32_t max_tiles = 0;
     uint32_t *d_sk0 = nullptr, *d_sk1 = nullptr, *d_sv0 = nullptr, *d_sv1 = nullptr;
     SegRec* d_heavy = nullptr;
+    // requests and results in sorted order (k_permute / k_unpermute)
+    int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
+    uint32_t* p_cfg = nullptr;
+    uint8_t* o_dec = nullptr;
+    int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
+    double* o_tok = nullptr;
     SegRec* d_light = nullptr;
     int replay_grid = 2048;
     uint32_t heavy_min = 32;   // segments this long replay cooperatively
@@ -219,6 +225,9 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_win);
     (void)hipFree(e->d_sk0); (void)hipFree(e->d_sk1); (void)hipFree(e->d_sv0); (void)hipFree(e->d_sv1);
     (void)hipFree(e->d_heavy);
+    (void)hipFree(e->p_ts); (void)hipFree(e->p_n); (void)hipFree(e->p_sms); (void)hipFree(e->p_cfg);
+    (void)hipFree(e->o_dec); (void)hipFree(e->o_rem); (void)hipFree(e->o_retry); (void)hipFree(e->o_reset);
+    (void)hipFree(e->o_tok);
     (void)hipFree(e->d_light);
     (void)hipFree(e->d_zero);
     (void)hipFree(e->d_eflags);
@@ -260,6 +269,15 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_sv0, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_sv1, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_heavy, sizeof(SegRec) * M) == hipSuccess;
+    ok &= hipMalloc(&e->p_ts, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->p_n, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->p_sms, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->p_cfg, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&e->o_dec, M) == hipSuccess;
+    ok &= hipMalloc(&e->o_rem, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->o_retry, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->o_reset, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->o_tok, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_light, sizeof(SegRec) * M) == hipSuccess;
     e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
     ok &= hipMalloc(&e->d_zero, e->zero_bytes) == hipSuccess;
@@ -372,10 +390,15 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
     k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->heavy_min, e->d_heavy, segctr, e->d_light,
                                       segctr + 1);
+    ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset,
+               a.tok ? e->o_tok : nullptr};
+    int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
+    k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, a, ps);
     if (e->timing) (void)hipEventRecord(ev[3], s);
-    k_replay<<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, vin, e->d_heavy, segctr, e->d_light, segctr + 1, segctr + 2,
-                                            e->win_base, e->d_tb, e->d_win, e->d_cfg, e->profile, a,
-                                            e->d_eflags, e->d_ctrl + CTRL_DBG);
+    k_replay<<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1, segctr + 2,
+                                                    e->win_base, e->d_tb, e->d_win, e->d_cfg, e->profile, ps,
+                                                    e->d_eflags, e->d_ctrl + CTRL_DBG);
+    k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, ps, a);
     if (e->timing) {
         (void)hipEventRecord(ev[4], s);
         e->ev_pending.push_back(ev);

@@ -52,34 +52,33 @@ __device__ inline uint32_t seg_end(const uint32_t* sk, uint32_t m, uint32_t j0, 
     return lo + 1;
 }
 
-// one request's inputs, loaded one step ahead of use (the loads of step j+1
-// are in flight while step j computes: the segment walk is a dependent chain
-// of gathers otherwise)
+// Replay kernels read the batch in SORTED order: k_permute has copied each
+// request's fields to position j of its segment (coalesced loads, one level)
+// and results are written at j (coalesced stores); k_unpermute moves them to
+// the caller's order.  ReqArgs here always points at the permuted buffers.
 struct Req {
-    uint32_t i;
     uint32_t c;
     int64_t t, n, sms;
 };
 
-__device__ inline Req load_req(const ReqArgs& a, const uint32_t* sv, uint32_t j) {
+__device__ inline Req load_req(const ReqArgs& a, uint32_t j) {
     Req r;
-    r.i = sv[j];
-    r.t = a.ts[r.i];
-    r.n = a.n[r.i];
-    r.c = a.cfg[r.i];
-    r.sms = a.sms ? a.sms[r.i] : floor_div(r.t, 1000000LL);
+    r.t = a.ts[j];
+    r.n = a.n[j];
+    r.c = a.cfg[j];
+    r.sms = a.sms[j];
     return r;
 }
 
-__device__ inline void replay_tb_serial(TbEntry* e, const uint32_t* sv, uint32_t j0, uint32_t j1,
-                                        const CfgDev* cfgs, int32_t profile, const ReqArgs& a) {
+__device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
+                                        int32_t profile, const ReqArgs& a) {
     TbState st{e->tok, e->last, e->when};
-    Req cur = load_req(a, sv, j0);
+    Req cur = load_req(a, j0);
     for (uint32_t j = j0; j < j1; j++) {
         Req nxt = cur;
-        if (j + 1 < j1) nxt = load_req(a, sv, j + 1);
+        if (j + 1 < j1) nxt = load_req(a, j + 1);
         Out o = tb_step(st, cur.t, cur.n, cur.sms, cfgs[cur.c], profile);
-        write_out(a, cur.i, o);
+        write_out(a, j, o);
         cur = nxt;
     }
     e->tok = st.tok;
@@ -87,21 +86,20 @@ __device__ inline void replay_tb_serial(TbEntry* e, const uint32_t* sv, uint32_t
     e->when = st.when;
 }
 
-__device__ inline void replay_win_serial(WinEntry* e, const uint32_t* sv, uint32_t j0, uint32_t j1,
-                                         const CfgDev* cfgs, int32_t profile, const ReqArgs& a,
-                                         uint32_t* eflags) {
+__device__ inline void replay_win_serial(WinEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
+                                         int32_t profile, const ReqArgs& a, uint32_t* eflags) {
     WinState w;
     w.s[0] = e->s[0];
     w.s[1] = e->s[1];
     uint32_t ef = 0;
-    Req cur = load_req(a, sv, j0);
+    Req cur = load_req(a, j0);
     for (uint32_t j = j0; j < j1; j++) {
         Req nxt = cur;
-        if (j + 1 < j1) nxt = load_req(a, sv, j + 1);
+        if (j + 1 < j1) nxt = load_req(a, j + 1);
         const CfgDev& c = cfgs[cur.c];
         Out o = (c.alg == ALG_SLIDING_WINDOW) ? sw_step(w, cur.t, cur.n, cur.sms, c, profile, ef)
                                               : fw_step(w, cur.t, cur.n, cur.sms, c, profile, ef);
-        write_out(a, cur.i, o);
+        write_out(a, j, o);
         cur = nxt;
     }
     e->s[0] = w.s[0];
@@ -216,7 +214,7 @@ __device__ inline int64_t wave_incl_scan_i64(int64_t v) {
 // One chunk's requests as the loader wave hands them to the compute waves.
 struct ChunkSlot {
     int64_t t, n, sms;
-    uint32_t i, c;
+    uint32_t c, pad;
 };
 
 struct CoopShared {
@@ -234,17 +232,17 @@ struct CoopShared {
 };
 
 // The replay block: COOP compute lanes (4 waves) + one loader wave.  The
-// loader is the only wave that issues the request gathers (sv -> ts, n, cfg,
-// server_ms), two chunks ahead, into an LDS ring.  On gfx9 loads and stores
+// loader is the only wave that loads the (sorted-order) request fields, two
+// chunks ahead, into an LDS ring.  On gfx9 loads and stores
 // share vmcnt, so a compute wave that both scattered results and waited on
 // its own prefetch would wait for its stores; here compute waves never wait
 // on global memory in the steady state.
 constexpr int REPLAY_BLOCK = COOP + 64;
 constexpr uint32_t NO_REQ = 0xffffffffu;
 
-__device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t* __restrict__ sv, uint32_t j0,
-                                      uint32_t j1, const CfgDev* __restrict__ cfgs, int32_t profile,
-                                      const ReqArgs& a, uint32_t* dbg) {
+__device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, uint32_t j0, uint32_t j1,
+                                      const CfgDev* __restrict__ cfgs, int32_t profile, const ReqArgs& a,
+                                      uint32_t* dbg) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
     const bool loader = wave == COOP_WAVES;
@@ -258,28 +256,20 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
         sh.carryL = e->last;
         sh.carryW = e->when;
     }
-    const uint32_t c0 = a.cfg[sv[j0]];
+    const uint32_t c0 = a.cfg[j0];
     const CfgDev cf0 = cfgs[c0];
-    // loader state: request indices of the next chunk (4 per loader lane)
-    uint32_t idx[4];
+    // loader state: requests of the chunk after next (4 per loader lane)
     ChunkSlot fld[4];
-    auto ld_idx = [&](uint32_t base) {
+    auto ld_fields = [&](uint32_t base) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             uint32_t j = base + lane + 64 * q;
-            idx[q] = (base < j1 && j < j1) ? sv[j] : NO_REQ;
-        }
-    };
-    auto ld_fields = [&]() {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint32_t i = idx[q];
-            ChunkSlot f{0, 1, 0, i, c0};
-            if (i != NO_REQ) {
-                f.t = a.ts[i];
-                f.n = a.n[i];
-                f.c = a.cfg[i];
-                f.sms = a.sms ? a.sms[i] : floor_div(f.t, 1000000LL);
+            ChunkSlot f{0, 1, 0, c0, 0};
+            if (base < j1 && j < j1) {
+                f.t = a.ts[j];
+                f.n = a.n[j];
+                f.c = a.cfg[j];
+                f.sms = a.sms[j];
             }
             fld[q] = f;
         }
@@ -288,11 +278,10 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
 #pragma unroll
         for (int q = 0; q < 4; q++) sh.ring[slot][lane + 64 * q] = fld[q];
     };
-    if (loader) {            // prologue: chunk 0 into slot 0, chunk 1's indices in flight
-        ld_idx(j0);
-        ld_fields();
+    if (loader) {            // prologue: chunk 0 into slot 0, chunk 1 in flight
+        ld_fields(j0);
         st_fields(0);
-        ld_idx(j0 + COOP);
+        ld_fields(j0 + COOP);
     }
     __syncthreads();
     uint32_t k = 0;
@@ -300,12 +289,8 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
         const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
         const bool act = !loader && tid < cnt;
         RL_STAMP(t0);
-        if (loader) {        // chunk k+1's fields, chunk k+2's indices: land during this chunk
-            ld_fields();
-            ld_idx(base + 2 * COOP);
-        }
-        ChunkSlot rq = loader ? ChunkSlot{0, 1, 0, NO_REQ, c0} : sh.ring[k & 1][tid];
-        const uint32_t i = rq.i;
+        ChunkSlot rq = loader ? ChunkSlot{0, 1, 0, c0, 0} : sh.ring[k & 1][tid];
+        const uint32_t i = base + tid;      // sorted position
         const int64_t t = rq.t, nn = rq.n, sms = rq.sms;
         const CfgDev cf = (rq.c == c0) ? cf0 : cfgs[rq.c];
         nchunks++;
@@ -442,7 +427,10 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, const uint32_t
             sh.carryL = Lq;
             sh.carryW = wafter;
         }
-        if (loader) st_fields((k + 1) & 1);   // chunk k+1 (loaded during this chunk's rounds)
+        if (loader) {        // chunk k+1 (loaded during this chunk) -> ring; start chunk k+2
+            st_fields((k + 1) & 1);
+            ld_fields(base + 2 * COOP);
+        }
         lds_barrier();
     }
     if (tid == 0) {
@@ -507,10 +495,40 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
     }
 }
 
+// requests in sorted order (one coalesced pass; random reads of the 28 B
+// request records, which stay in the Infinity Cache at 1M-request batches)
+__global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                                 uint32_t m, uint32_t invalid_key, ReqArgs in, ReqArgs out) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+        if (sk[j] == invalid_key) continue;
+        uint32_t i = sv[j];
+        int64_t t = in.ts[i];
+        // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
+        const_cast<int64_t*>(out.ts)[j] = t;
+        const_cast<int64_t*>(out.n)[j] = in.n[i];
+        const_cast<uint32_t*>(out.cfg)[j] = in.cfg[i];
+        const_cast<int64_t*>(out.sms)[j] = in.sms ? in.sms[i] : floor_div(t, 1000000LL);
+    }
+}
+
+// results from sorted order back to the caller's order
+__global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                                   uint32_t m, uint32_t invalid_key, ReqArgs sorted, ReqArgs out) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+        if (sk[j] == invalid_key) continue;
+        uint32_t i = sv[j];
+        out.dec[i] = sorted.dec[j];
+        out.rem[i] = sorted.rem[j];
+        out.retry[i] = sorted.retry[j];
+        out.reset[i] = sorted.reset[j];
+        if (out.tok) out.tok[i] = sorted.tok[j];
+    }
+}
+
 // Work-queue replay: blocks first drain the heavy list (one segment per block,
 // cooperative), then the light list (256 segments per grab, one per thread).
 __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
-    const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv, const SegRec* __restrict__ heavy,
+    const uint32_t* __restrict__ sk, const SegRec* __restrict__ heavy,
     const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
     const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
     const CfgDev* __restrict__ cfgs, int32_t profile, ReqArgs a, uint32_t* eflags, uint32_t* dbg) {
@@ -526,9 +544,9 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
         const SegRec sg = heavy[u];
         const uint32_t k0 = sk[sg.j0];
         if (k0 < win_base) {
-            replay_tb_coop(sh, &tb[k0], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a, dbg);
+            replay_tb_coop(sh, &tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, dbg);
         } else if (threadIdx.x == 0) {
-            replay_win_serial(&win[k0 - win_base], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+            replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
         __syncthreads();
     }
@@ -542,8 +560,8 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
         if (u < nlight) {
             const SegRec sg = light[u];
             const uint32_t k0 = sk[sg.j0];
-            if (k0 < win_base) replay_tb_serial(&tb[k0], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a);
-            else replay_win_serial(&win[k0 - win_base], sv, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a);
+            else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
     }
 }
