@@ -395,9 +395,15 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
     k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, a, ps);
     if (e->timing) (void)hipEventRecord(ev[3], s);
-    k_replay<<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1, segctr + 2,
-                                                    e->win_base, e->d_tb, e->d_win, e->d_cfg, e->profile, ps,
-                                                    e->d_eflags, e->d_ctrl + CTRL_DBG);
+    const uint32_t ncfg = (uint32_t)e->h_cfg.size();
+    if (ncfg <= (uint32_t)MAX_LCFG)
+        k_replay<true><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
+                                                              segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
+                                                              ncfg, e->profile, ps, e->d_eflags, e->d_ctrl + CTRL_DBG);
+    else
+        k_replay<false><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
+                                                               segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
+                                                               ncfg, e->profile, ps, e->d_eflags, e->d_ctrl + CTRL_DBG);
     k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, ps, a);
     if (e->timing) {
         (void)hipEventRecord(ev[4], s);

@@ -283,7 +283,17 @@ RL_INLINE bool dec14_fast(double a, int64_t& D, int& E) {
     return true;
 }
 
-RL_COLD void dec14_slow(double a, int64_t& D, int& E) {
+struct Dec14 {
+    int64_t D;
+    int E;
+};
+
+// returned by value (registers): out-parameters of an out-of-line call would
+// round-trip through scratch, and scratch loads share vmcnt with the caller's
+// pending stores (every join after the call would wait for them)
+RL_COLD Dec14 dec14_slow_v(double a) {
+    int64_t D;
+    int E;
     uint64_t bits = dbits(a);
     int ex = (int)((bits >> 52) & 0x7ff);
     uint64_t m = bits & ((1ULL << 52) - 1);
@@ -294,9 +304,16 @@ RL_COLD void dec14_slow(double a, int64_t& D, int& E) {
     int E0 = floor_log10_pow2(e2);
     const int64_t LO = 10000000000000LL, HI = 100000000000000LL;
     int64_t D1 = round_scaled_big(m, e, 12 - E0);
-    if (D1 >= LO) { D = D1; E = E0 + 1; return; }
+    if (D1 >= LO) return Dec14{D1, E0 + 1};
     int64_t D0 = round_scaled_big(m, e, 13 - E0);
     if (D0 >= HI) { D = LO; E = E0 + 1; } else { D = D0; E = E0; }
+    return Dec14{D, E};
+}
+
+RL_INLINE void dec14_slow(double a, int64_t& D, int& E) {
+    Dec14 r = dec14_slow_v(a);
+    D = r.D;
+    E = r.E;
 }
 
 // strtod of D * 10^(E-13), D < 2^47

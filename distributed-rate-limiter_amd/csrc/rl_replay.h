@@ -217,6 +217,9 @@ struct ChunkSlot {
     uint32_t c, pad;
 };
 
+// configs cached in LDS per block (when the engine has at most MAX_LCFG)
+constexpr int MAX_LCFG = 32;
+
 struct CoopShared {
     ChunkSlot ring[2][COOP];  // requests of chunk k (slot k&1), filled by the loader wave
     double L[COOP];           // stored last_refill after each lane's step
@@ -256,20 +259,21 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, uint32_t j0, u
         sh.carryL = e->last;
         sh.carryW = e->when;
     }
-    const uint32_t c0 = a.cfg[j0];
-    const CfgDev cf0 = cfgs[c0];
-    // loader state: requests of the chunk after next (4 per loader lane)
+    // loader state: requests of the chunk after next (4 per loader lane).
+    // Compute waves read only LDS (ring + config cache): on gfx9 a wait on any
+    // global load would also wait for the result stores they keep in flight
+    // (loads and stores share vmcnt).
     ChunkSlot fld[4];
     auto ld_fields = [&](uint32_t base) {
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             uint32_t j = base + lane + 64 * q;
-            ChunkSlot f{0, 1, 0, c0, 0};
+            ChunkSlot f{0, 1, 0, 0, 0};
             if (base < j1 && j < j1) {
                 f.t = a.ts[j];
                 f.n = a.n[j];
-                f.c = a.cfg[j];
                 f.sms = a.sms[j];
+                f.c = a.cfg[j];
             }
             fld[q] = f;
         }
@@ -289,10 +293,10 @@ __device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, uint32_t j0, u
         const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
         const bool act = !loader && tid < cnt;
         RL_STAMP(t0);
-        ChunkSlot rq = loader ? ChunkSlot{0, 1, 0, c0, 0} : sh.ring[k & 1][tid];
+        ChunkSlot rq = loader ? ChunkSlot{0, 1, 0, 0, 0} : sh.ring[k & 1][tid];
         const uint32_t i = base + tid;      // sorted position
         const int64_t t = rq.t, nn = rq.n, sms = rq.sms;
-        const CfgDev cf = (rq.c == c0) ? cf0 : cfgs[rq.c];
+        const CfgDev& cf = cfgs[rq.c];      // LDS copy (see k_replay)
         nchunks++;
         const double now = (double)t / 1e9;
         const double Lq = act ? lua_tostring_roundtrip(now, profile) : 0.0;
@@ -527,13 +531,21 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
 
 // Work-queue replay: blocks first drain the heavy list (one segment per block,
 // cooperative), then the light list (256 segments per grab, one per thread).
+template <bool LCFG>
 __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     const uint32_t* __restrict__ sk, const SegRec* __restrict__ heavy,
     const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
     const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
-    const CfgDev* __restrict__ cfgs, int32_t profile, ReqArgs a, uint32_t* eflags, uint32_t* dbg) {
+    const CfgDev* __restrict__ gcfgs, uint32_t ncfg, int32_t profile, ReqArgs a, uint32_t* eflags,
+    uint32_t* dbg) {
     __shared__ CoopShared sh;
     __shared__ uint32_t s_u;
+    __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
+    if (LCFG) {
+        for (uint32_t c = threadIdx.x; c < ncfg; c += blockDim.x) s_cfg[c] = gcfgs[c];
+        __syncthreads();
+    }
+    const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
     const uint32_t nheavy = *nheavy_p, nlight = *nlight_p;
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
