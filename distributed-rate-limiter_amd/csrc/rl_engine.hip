@@ -180,6 +180,10 @@ struct rl_engine {
     uint8_t* o_dec = nullptr;
     int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
     double* o_tok = nullptr;
+    // token-bucket precomputation (k_permute)
+    double *q_add = nullptr, *q_lq = nullptr;
+    int64_t *q_reset = nullptr, *q_when = nullptr;
+    uint8_t* q_alive = nullptr;
     SegRec* d_light = nullptr;
     int replay_grid = 2048;
     uint32_t heavy_min = 32;   // segments this long replay cooperatively
@@ -228,6 +232,8 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->p_ts); (void)hipFree(e->p_n); (void)hipFree(e->p_sms); (void)hipFree(e->p_cfg);
     (void)hipFree(e->o_dec); (void)hipFree(e->o_rem); (void)hipFree(e->o_retry); (void)hipFree(e->o_reset);
     (void)hipFree(e->o_tok);
+    (void)hipFree(e->q_add); (void)hipFree(e->q_lq); (void)hipFree(e->q_reset); (void)hipFree(e->q_when);
+    (void)hipFree(e->q_alive);
     (void)hipFree(e->d_light);
     (void)hipFree(e->d_zero);
     (void)hipFree(e->d_eflags);
@@ -278,6 +284,11 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->o_retry, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_tok, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->q_add, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->q_lq, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->q_reset, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->q_when, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->q_alive, M) == hipSuccess;
     ok &= hipMalloc(&e->d_light, sizeof(SegRec) * M) == hipSuccess;
     e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
     ok &= hipMalloc(&e->d_zero, e->zero_bytes) == hipSuccess;
@@ -393,17 +404,21 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset,
                a.tok ? e->o_tok : nullptr};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
-    k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, a, ps);
+    TbPre pre{e->q_add, e->q_reset, e->q_lq, e->q_when, e->q_alive};
+    k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_tb, e->d_cfg, e->profile, a, ps,
+                                    pre);
     if (e->timing) (void)hipEventRecord(ev[3], s);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     if (ncfg <= (uint32_t)MAX_LCFG)
         k_replay<true><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                               segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
-                                                              ncfg, e->profile, ps, e->d_eflags, e->d_ctrl + CTRL_DBG);
+                                                              ncfg, e->profile, ps, pre, e->d_eflags,
+                                                              e->d_ctrl + CTRL_DBG);
     else
         k_replay<false><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                                segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
-                                                               ncfg, e->profile, ps, e->d_eflags, e->d_ctrl + CTRL_DBG);
+                                                               ncfg, e->profile, ps, pre, e->d_eflags,
+                                                              e->d_ctrl + CTRL_DBG);
     k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, ps, a);
     if (e->timing) {
         (void)hipEventRecord(ev[4], s);

@@ -28,6 +28,17 @@ struct ReqArgs {
     double* tok;          // nullable
 };
 
+// State-independent token-bucket quantities of each request (sorted order),
+// computed in the permute pass: the previous request of the same key is the
+// previous sorted position (or, for a segment head, the table entry).
+struct TbPre {
+    double* add;       // elapsed * refill_rate (tokenbucket.go:36-37)
+    int64_t* reset;    // calculateResetTime (tokenbucket.go:161-165)
+    double* lq;        // tostring(now) as stored in last_refill (tokenbucket.go:48)
+    int64_t* when;     // key expiry after this request's EXPIRE (tokenbucket.go:49)
+    uint8_t* alive;    // did HMGET see the key (tokenbucket.go:31-33)
+};
+
 __device__ inline int64_t req_server_ms(const ReqArgs& a, uint32_t i, int64_t t) {
     return a.sms ? a.sms[i] : floor_div(t, 1000000LL);
 }
@@ -70,20 +81,43 @@ __device__ inline Req load_req(const ReqArgs& a, uint32_t j) {
     return r;
 }
 
-__device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
-                                        int32_t profile, const ReqArgs& a) {
-    TbState st{e->tok, e->last, e->when};
-    Req cur = load_req(a, j0);
-    for (uint32_t j = j0; j < j1; j++) {
-        Req nxt = cur;
-        if (j + 1 < j1) nxt = load_req(a, j + 1);
-        Out o = tb_step(st, cur.t, cur.n, cur.sms, cfgs[cur.c], profile);
-        write_out(a, j, o);
-        cur = nxt;
+// one token-bucket script execution on precomputed inputs (tb_step's
+// state-dependent part: tokenbucket.go:32-51 + 114-130)
+__device__ inline Out tb_chain_step(double& tok, bool alive, double add, int64_t n, int64_t reset_at,
+                                    const CfgDev& c, int32_t profile) {
+    Out o;
+    const double capacity = c.limit_d;
+    double tokens = alive ? tok : capacity;
+    double sum = tokens + add;
+    tokens = (sum < capacity) ? sum : capacity;           // math.min(capacity, sum)
+    bool allowed = false;
+    if (tokens >= (double)n) { tokens = tokens - (double)n; allowed = true; }
+    tok = lua_tostring_roundtrip(tokens, profile);
+    int64_t rem = go_f2i(floor(tokens));
+    o.tokens = tokens;
+    o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
+    o.remaining = rem;
+    o.reset_at = reset_at;
+    o.retry = 0;
+    if (!allowed) {
+        int64_t need = wsub(n, rem);
+        double w = need == 1 ? c.inv_rate : (double)need / c.rate;   // tokensNeeded / refillRate
+        int64_t d = go_f2i(w * 1e9);
+        o.retry = d < 0 ? 0 : d;
     }
-    e->tok = st.tok;
-    e->last = st.last;
-    e->when = st.when;
+    return o;
+}
+
+__device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
+                                        int32_t profile, const ReqArgs& a, const TbPre& pre) {
+    double tok = e->tok;
+    for (uint32_t j = j0; j < j1; j++) {
+        Out o = tb_chain_step(tok, pre.alive[j] != 0, pre.add[j], a.n[j], pre.reset[j], cfgs[a.cfg[j]], profile);
+        write_out(a, j, o);
+    }
+    e->tok = tok;
+    e->last = pre.lq[j1 - 1];
+    e->when = pre.when[j1 - 1];
 }
 
 __device__ inline void replay_win_serial(WinEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
@@ -130,8 +164,6 @@ __device__ inline void replay_win_serial(WinEntry* e, uint32_t j0, uint32_t j1, 
 // The result is identical to serial replay by construction; the common case
 // (denied requests accumulating refill) commits 256 steps per round.
 // ---------------------------------------------------------------------------
-constexpr int COOP = 256;
-constexpr int COOP_WAVES = COOP / 64;
 
 struct TbQ {
     int64_t D;
@@ -211,241 +243,363 @@ __device__ inline int64_t wave_incl_scan_i64(int64_t v) {
     return v;
 }
 
-// One chunk's requests as the loader wave hands them to the compute waves.
+// ---------------------------------------------------------------------------
+// In-round flip resolution.
+//
+// Within a decade (Redis profile) or binade (miniredis profile) the stored
+// state is an integer D, and a step maps D to D + r_j, r_j = round(add_j / u),
+// except when add_j / u lies within TAU of a half-integer: then the IEEE
+// rounding of T = strtod(D) and of T + add (|error| <= 0.0222 u, SURVEY-level
+// bound 10^14 * 2^-52) can flip the rounded result by one.  So a lane whose
+// fraction is far from 1/2 maps a predecessor error c to the same c; only
+// near-tie lanes depend on the exact predecessor.  One round:
+//   1. nominal r_j, near-tie flag; block scan of r (DPP) -> nominal
+//      predecessor D + P_j; compaction rank of the near-tie lanes,
+//   2. first lane e where an event (allow, clamp, decade change, expired key,
+//      > 64 near lanes) is possible even with |c| <= 2,
+//   3. every near-tie lane before e is evaluated EXACTLY for the five
+//      candidate predecessors D + P_j + c, c in [-2, 2] (one (lane, c) pair
+//      per thread): a table c -> c' (or STOP),
+//   4. one wave composes the tables (a function-composition scan) -> the true
+//      correction after each near-tie lane; a STOP shortens the round,
+//   5. every lane up to e runs the step EXACTLY from its now-known true
+//      predecessor and checks the result it implies; the first mismatch (none
+//      if the bound holds) also ends the round -- correctness never rests on
+//      the bound, only the speed does,
+//   6. lanes up to e are committed; e's exact result is the next base.
+// Rounds per chunk = 1 + events, not 1 + flips.
+// ---------------------------------------------------------------------------
+
+// One chunk's requests as the loader wave hands them to the compute waves
+// (state-independent terms precomputed by k_permute).
 struct ChunkSlot {
-    int64_t t, n, sms;
-    uint32_t c, pad;
+    double add;
+    int64_t n;
+    int64_t reset;
+    uint32_t c;
+    uint32_t alive;
 };
 
 // configs cached in LDS per block (when the engine has at most MAX_LCFG)
 constexpr int MAX_LCFG = 32;
+constexpr int MAX_NEAR = 64;
+constexpr uint32_t STOPC = 7;
+constexpr double TAU_DEC = 0.03;   // > 0.0222: far lanes are exact by the bound
 
-struct CoopShared {
-    ChunkSlot ring[2][COOP];  // requests of chunk k (slot k&1), filled by the loader wave
-    double L[COOP];           // stored last_refill after each lane's step
-    int64_t W[COOP];          // key expiry after each lane's step
-    int64_t scan_tmp[COOP_WAVES];
-    uint32_t min_tmp[COOP_WAVES];
-    int64_t baseD;
-    int32_t baseE;
-    uint32_t need_full;       // committed lane must re-quantize its tokens
-    double carryL;
-    int64_t carryW;
-    double full_tokens;
+enum : int { QM_NONE = 0, QM_DEC = 1, QM_BIN = 2 };
+
+struct TbEval {
+    double tokens;
+    bool allowed;
+    bool clamped;
+    bool inrange;   // Dact is the canonical stored representation in this decade
+    int64_t Dact;
 };
 
-// The replay block: COOP compute lanes (4 waves) + one loader wave.  The
-// loader is the only wave that loads the (sorted-order) request fields, two
-// chunks ahead, into an LDS ring.  On gfx9 loads and stores
-// share vmcnt, so a compute wave that both scattered results and waited on
-// its own prefetch would wait for its stores; here compute waves never wait
-// on global memory in the steady state.
-constexpr int REPLAY_BLOCK = COOP + 64;
-constexpr uint32_t NO_REQ = 0xffffffffu;
+// the script step from a stored state given as digits Dpred in (mode, E)
+__device__ inline TbEval tb_eval(int mode, int64_t Dpred, int32_t E, double P, double R, bool alive, double add,
+                                 double cap, double nd, int32_t profile) {
+    TbEval v;
+    double T;
+    if (!alive) T = cap;
+    else if (mode == QM_DEC) T = rlq::div_pow10((double)Dpred, P, R);   // strtod("D e(E-13)")
+    else if (mode == QM_BIN) T = (double)Dpred * R;                      // exact: R = 2^E
+    else T = tb_value(Dpred, E, profile);
+    const double sum = T + add;
+    v.clamped = !(sum < cap);
+    double tokens = v.clamped ? cap : sum;                               // math.min(capacity, sum)
+    v.allowed = tokens >= nd;
+    if (v.allowed) tokens = tokens - nd;
+    v.tokens = tokens;
+    v.Dact = 0;
+    v.inrange = false;
+    if (mode == QM_DEC) {
+        if (tokens > 0.0 && tokens * P < 1.4e14) {
+            v.Dact = rlq::round_scaled_P(tokens, P);
+            v.inrange = v.Dact >= 10000000000000LL && v.Dact < 100000000000000LL;
+        }
+    } else if (mode == QM_BIN) {
+        const double w = tokens * P;                                     // exact scaling
+        if (w >= 4503599627370496.0 && w < 9007199254740992.0) {
+            v.Dact = (int64_t)w;
+            v.inrange = (double)v.Dact == w;
+        }
+    }
+    return v;
+}
 
-__device__ inline void replay_tb_coop(CoopShared& sh, TbEntry* e, uint32_t j0, uint32_t j1,
+__device__ inline Out tb_outputs(const TbEval& v, int64_t nn, int64_t reset_at, double rate, double inv_rate) {
+    Out o;
+    const int64_t rem = go_f2i(floor(v.tokens));
+    o.tokens = v.tokens;
+    o.decision = v.allowed ? DEC_ALLOWED : DEC_DENIED;
+    o.remaining = rem;
+    o.reset_at = reset_at;
+    o.retry = 0;
+    if (!v.allowed) {
+        const int64_t need = wsub(nn, rem);
+        // tokensNeeded / refillRate (tokenbucket.go:124-126); 1/rate precomputed
+        const double w = need == 1 ? inv_rate : (double)need / rate;
+        const int64_t d = go_f2i(w * 1e9);
+        o.retry = d < 0 ? 0 : d;
+    }
+    return o;
+}
+
+__device__ inline uint32_t pack_ident() {   // identity table: c -> c
+    uint32_t f = 0;
+    for (int k = 0; k < 5; k++) f |= (uint32_t)k << (3 * k);
+    return f;
+}
+// (f after g): apply g first, then f
+__device__ inline uint32_t compose(uint32_t f, uint32_t g) {
+    uint32_t h = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        uint32_t gk = (g >> (3 * k)) & 7u;
+        uint32_t hk = gk == STOPC ? STOPC : ((f >> (3 * gk)) & 7u);
+        h |= hk << (3 * k);
+    }
+    return h;
+}
+
+template <int NC>
+struct CoopShared {
+    ChunkSlot ring[2][NC];            // chunk k in slot k&1, filled by the loader wave
+    int64_t wtot[NC / 64];
+    uint64_t wnear[NC / 64];
+    uint32_t wev[NC / 64];
+    uint32_t wbad[NC / 64];
+    double nadd[MAX_NEAR], ncap[MAX_NEAR], nnd[MAX_NEAR];
+    int64_t npred[MAX_NEAR], nr[MAX_NEAR];
+    uint32_t nlane[MAX_NEAR];
+    uint8_t ntab[MAX_NEAR * 5];
+    int8_t cafter[MAX_NEAR];
+    uint32_t stop_lane;
+    int64_t baseD;
+    int32_t baseE;
+};
+
+template <int NC>
+__device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j0, uint32_t j1,
                                       const CfgDev* __restrict__ cfgs, int32_t profile, const ReqArgs& a,
-                                      uint32_t* dbg) {
+                                      const TbPre& pre, uint32_t* dbg) {
+    constexpr int NWC = NC / 64;                 // compute waves
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63, wave = tid >> 6;
-    const bool loader = wave == COOP_WAVES;
+    const bool loader = wave == (uint32_t)NWC;
+    const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t nrounds = 0, nchunks = 0;
-    uint64_t cyc[5] = {0, 0, 0, 0, 0}, t0 = 0, t1 = 0;
-    (void)cyc; (void)t0; (void)t1;
     if (tid == 0) {
         TbQ q = tb_quant(e->tok, profile);
         sh.baseD = q.D;
         sh.baseE = q.E;
-        sh.carryL = e->last;
-        sh.carryW = e->when;
     }
-    // loader state: requests of the chunk after next (4 per loader lane).
-    // Compute waves read only LDS (ring + config cache): on gfx9 a wait on any
-    // global load would also wait for the result stores they keep in flight
-    // (loads and stores share vmcnt).
-    ChunkSlot fld[4];
+    // loader: the chunk after next, NC/64 entries per loader lane
+    ChunkSlot fld[NWC];
     auto ld_fields = [&](uint32_t base) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            uint32_t j = base + lane + 64 * q;
-            ChunkSlot f{0, 1, 0, 0, 0};
+        for (int q = 0; q < NWC; q++) {
+            const uint32_t j = base + lane + 64 * q;
+            ChunkSlot f{0.0, 1, 0, 0, 0};
             if (base < j1 && j < j1) {
-                f.t = a.ts[j];
+                f.add = pre.add[j];
                 f.n = a.n[j];
-                f.sms = a.sms[j];
+                f.reset = pre.reset[j];
                 f.c = a.cfg[j];
+                f.alive = pre.alive[j];
             }
             fld[q] = f;
         }
     };
     auto st_fields = [&](int slot) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) sh.ring[slot][lane + 64 * q] = fld[q];
+        for (int q = 0; q < NWC; q++) sh.ring[slot][lane + 64 * q] = fld[q];
     };
-    if (loader) {            // prologue: chunk 0 into slot 0, chunk 1 in flight
+    if (loader) {
         ld_fields(j0);
         st_fields(0);
-        ld_fields(j0 + COOP);
+        ld_fields(j0 + NC);
     }
     __syncthreads();
     uint32_t k = 0;
-    for (uint32_t base = j0; base < j1; base += COOP, k++) {
-        const uint32_t cnt = (j1 - base) < (uint32_t)COOP ? (j1 - base) : (uint32_t)COOP;
+    for (uint32_t base = j0; base < j1; base += NC, k++) {
+        const uint32_t cnt = (j1 - base) < (uint32_t)NC ? (j1 - base) : (uint32_t)NC;
         const bool act = !loader && tid < cnt;
-        RL_STAMP(t0);
-        ChunkSlot rq = loader ? ChunkSlot{0, 1, 0, 0, 0} : sh.ring[k & 1][tid];
-        const uint32_t i = base + tid;      // sorted position
-        const int64_t t = rq.t, nn = rq.n, sms = rq.sms;
-        const CfgDev& cf = cfgs[rq.c];      // LDS copy (see k_replay)
+        const ChunkSlot rq = loader ? ChunkSlot{0.0, 1, 0, 0, 0} : sh.ring[k & 1][tid];
+        const uint32_t i = base + tid;     // sorted position
+        const CfgDev& cf = cfgs[rq.c];     // LDS copy (see k_replay)
+        const double add = rq.add, cap = cf.limit_d, nd = (double)rq.n;
+        const bool alive = rq.alive != 0;
         nchunks++;
-        const double now = (double)t / 1e9;
-        const double Lq = act ? lua_tostring_roundtrip(now, profile) : 0.0;
-        const int64_t wafter = expire_when(cf.ttl_tb, sms);
-        const int64_t reset_at = tb_reset_at(now, cf);
-        if (!loader) {
-            sh.L[tid] = Lq;
-            sh.W[tid] = wafter;
-        }
-        lds_barrier();
-        const uint32_t pv = (tid > 0 && tid < (uint32_t)COOP) ? tid - 1 : 0;
-        const double prevL = tid ? sh.L[pv] : sh.carryL;
-        const int64_t prevW = tid ? sh.W[pv] : sh.carryW;
-        const bool alive = key_alive(prevW, sms, profile);
-        const double last = alive ? prevL : now;
-        const double add = (now - last) * cf.rate;     // elapsed * refill_rate
-        const double cap = cf.limit_d, nd = (double)nn, rate = cf.rate, inv_rate = cf.inv_rate;
-        RL_STAMP(t1);
-#ifdef RL_STAMPS
-        cyc[0] += t1 - t0;
-#endif
         uint32_t first = 0;
-        int32_t scaleE = INT32_MIN;
-        double scale = 0.0, P = 1.0, R = 1.0;
-        bool fastdec = false;
-        while (first < cnt) {                           // block-uniform
+        while (first < cnt) {              // block-uniform
+            nrounds++;
             const int64_t D = sh.baseD;
             const int32_t E = sh.baseE;
+            int mode = QM_NONE;
+            double P = 1.0, R = 1.0, tau = 0.0;
+            if (profile == PROFILE_REDIS7) {
+                if (13 - E >= 1 && 13 - E <= 22 && D >= 10000000000000LL && D < 100000000000000LL) {
+                    mode = QM_DEC;
+                    P = rlq::pow10_exact(13 - E);
+                    R = 1.0 / P;
+                    tau = TAU_DEC;
+                }
+            } else if (D >= (1LL << 52) && D < (1LL << 53) && E > -1000 && E < 900) {
+                mode = QM_BIN;
+                P = ldexp(1.0, -E);
+                R = ldexp(1.0, E);
+            }
             const bool mine = act && tid >= first;
-            nrounds++;
-            if (E != scaleE) {
-                scaleE = E;
-                scale = tb_scale(E, profile);
-                // Redis profile, decade with an exact power of ten: short chain
-                fastdec = profile == PROFILE_REDIS7 && (13 - E) >= 1 && (13 - E) <= 22;
-                if (fastdec) { P = rlq::pow10_exact(13 - E); R = 1.0 / P; }
+            if (mode == QM_NONE) {
+                // off the fast decades (or an empty/zero state): one exact step
+                if (tid == first) {
+                    TbEval v = tb_eval(QM_NONE, D, E, P, R, alive, add, cap, nd, profile);
+                    write_out(a, i, tb_outputs(v, rq.n, rq.reset, cf.rate, cf.inv_rate));
+                    TbQ q = tb_quant(v.tokens, profile);
+                    sh.baseD = q.D;
+                    sh.baseE = q.E;
+                }
+                lds_barrier();
+                first++;
+                continue;
             }
+            // 1. nominal increment, near-tie flag, event flags that need no prefix
             int64_t r = 0;
-            bool force = !alive;
+            bool near = false, ev = !alive;
             if (mine) {
-                double v = add * scale;
-                if (!(v < 1e15 && v > -1e15)) force = true;
-                else r = (int64_t)rint(v);
+                const double pr = add * P;
+                const double err = (mode == QM_DEC) ? __builtin_fma(add, P, -pr) : 0.0;
+                const double rr = rint(pr);
+                if (!(pr < 1e15 && pr > -1e15)) {
+                    ev = true;
+                } else {
+                    r = (int64_t)rr;
+                    const double dist = fabs((pr - rr) + err);       // distance to nearest integer
+                    near = (mode == QM_DEC) ? dist > 0.5 - tau : dist >= 0.5;
+                }
             }
-            // exclusive block scan of r: DPP within the wave, wave totals via LDS
-            RL_STAMP(t0);
             const int64_t rin = mine ? r : 0;
             const int64_t inc = wave_incl_scan_i64(rin);
-            if (lane == 63 && !loader) sh.scan_tmp[wave] = inc;
-            lds_barrier();                                               // A
-            int64_t pre = 0;
-            for (uint32_t w = 0; w < wave && w < (uint32_t)COOP_WAVES; w++) pre += sh.scan_tmp[w];
-            const int64_t Dg = D + pre + inc - rin;
-            RL_STAMP(t1);
-#ifdef RL_STAMPS
-            cyc[1] += t1 - t0; t0 = t1;
-#endif
-            bool ok = false, full = false;
-            Out o;
-            TbQ q{0, 0};
-            double tokens = 0.0;
-            if (mine) {
-                // tokenBucketScript from the guessed stored state (tokenbucket.go:32-51)
-                double T;
-                if (!alive) T = cap;
-                else if (fastdec && Dg > 0) T = rlq::div_pow10((double)Dg, P, R);   // == strtod(D e(E-13))
-                else T = tb_value(Dg, E, profile);
-                double sum = T + add;
-                tokens = (sum < cap) ? sum : cap;
-                bool allowed = false;
-                if (tokens >= nd) { tokens = tokens - nd; allowed = true; }
-                // tonumber(tostring(tokens)) as (digits, decade), and is it the guess?
-                const int64_t Dexp = Dg + r;
-                if (fastdec && tokens > 0.0 && tokens * P < 1.4e14) {
-                    const int64_t Dact = rlq::round_scaled_P(tokens, P);
-                    const bool inrange = Dact >= 10000000000000LL && Dact < 100000000000000LL;
-                    ok = !force && inrange && Dact == Dexp;
-                    full = !inrange;
-                    q = TbQ{Dact, E};
-                } else if (profile != PROFILE_REDIS7) {
-                    int64_t ad = Dexp < 0 ? -Dexp : Dexp;
-                    ok = !force && ad >= (1LL << 52) && ad < (1LL << 53) && tokens == ldexp((double)Dexp, E);
-                    full = !ok;
-                    q = TbQ{Dexp, E};
-                } else {
-                    full = true;    // off the fast decades: quantize in full if this lane commits
-                }
-                int64_t rem = go_f2i(floor(tokens));
-                o.tokens = tokens;
-                o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
-                o.remaining = rem;
-                o.reset_at = reset_at;
-                o.retry = 0;
-                if (!allowed) {
-                    int64_t need = wsub(nn, rem);
-                    // tokensNeeded / refillRate (tokenbucket.go:124-126); 1/rate precomputed
-                    double w = need == 1 ? inv_rate : (double)need / rate;
-                    int64_t d = go_f2i(w * 1e9);
-                    o.retry = d < 0 ? 0 : d;
-                }
+            const uint64_t nmask = __ballot(mine && near);
+            if (!loader) {
+                if (lane == 63) sh.wtot[wave] = inc;
+                if (lane == 0) sh.wnear[wave] = nmask;
             }
-            RL_STAMP(t1);
-#ifdef RL_STAMPS
-            cyc[2] += t1 - t0; t0 = t1;
-#endif
-            // first lane whose exact result differs from its guess
-            const uint64_t bad = __ballot(mine && !ok);
-            if (lane == 0 && !loader)
-                sh.min_tmp[wave] = bad ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bad) - 1) : COOP;
-            lds_barrier();                                               // B
-            uint32_t s = COOP;
-            for (int w = 0; w < COOP_WAVES; w++) s = sh.min_tmp[w] < s ? sh.min_tmp[w] : s;
-            if (s >= cnt) s = cnt - 1;
-            RL_STAMP(t1);
-#ifdef RL_STAMPS
-            cyc[3] += t1 - t0; t0 = t1;
-#endif
-            if (mine && tid <= s) write_out(a, i, o);
-            if (tid == s) {
-                if (full) q = tb_quant(tokens, profile);   // decade change, allow, zero, slow path
+            lds_barrier();                                                   // 1
+            int64_t pre_sum = 0;
+            uint32_t nbefore = 0;
+            for (uint32_t w = 0; w < wave && w < (uint32_t)NWC; w++) {
+                pre_sum += sh.wtot[w];
+                nbefore += (uint32_t)__popcll(sh.wnear[w]);
+            }
+            const int64_t Pj = pre_sum + inc - rin;                          // exclusive prefix
+            const uint32_t nrank = nbefore + (loader ? 0u : (uint32_t)__popcll(nmask & lt));
+            // 2. events possible even with |c| <= 2
+            if (mine && !ev) {
+                const int64_t Dn = D + Pj + r;
+                const int64_t M = 4;
+                if (mode == QM_DEC) ev = (Dn - M < 10000000000000LL) || (Dn + M >= 100000000000000LL);
+                else ev = (Dn - M < (1LL << 52)) || (Dn + M >= (1LL << 53));
+                const double vhi = (double)(Dn + M) * R * (1.0 + 1e-9);
+                ev = ev || vhi >= nd || vhi >= cap || (near && nrank >= (uint32_t)MAX_NEAR);
+            }
+            const uint64_t emask = __ballot(mine && ev);
+            if (!loader && lane == 0)
+                sh.wev[wave] = emask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)emask) - 1) : (uint32_t)NC;
+            lds_barrier();                                                   // 2
+            uint32_t eidx = NC;
+            for (int w = 0; w < NWC; w++) eidx = sh.wev[w] < eidx ? sh.wev[w] : eidx;
+            if (eidx >= cnt) eidx = cnt - 1;
+            // near-tie lanes strictly before e: publish their inputs
+            uint32_t NN = 0;
+            {
+                const uint32_t ew = eidx >> 6, el = eidx & 63;
+                for (uint32_t w = 0; w < ew; w++) NN += (uint32_t)__popcll(sh.wnear[w]);
+                NN += (uint32_t)__popcll(sh.wnear[ew] & ((1ull << el) - 1ull));
+            }
+            if (mine && near && tid < eidx) {
+                sh.nadd[nrank] = add;
+                sh.ncap[nrank] = cap;
+                sh.nnd[nrank] = nd;
+                sh.npred[nrank] = D + Pj;
+                sh.nr[nrank] = r;
+                sh.nlane[nrank] = tid;
+            }
+            lds_barrier();                                                   // 3
+            // 3. candidate tables: one (near lane, c) pair per compute thread
+            if (!loader && tid < NN * 5) {
+                const uint32_t rk = tid / 5;
+                const int32_t cc = (int32_t)(tid % 5) - 2;
+                const int64_t base_pred = sh.npred[rk];
+                TbEval v = tb_eval(mode, base_pred + cc, E, P, R, true, sh.nadd[rk], sh.ncap[rk], sh.nnd[rk],
+                                   profile);
+                uint32_t entry = STOPC;
+                if (v.inrange && !v.allowed && !v.clamped) {
+                    const int64_t cp = v.Dact - (base_pred + sh.nr[rk]);
+                    if (cp >= -2 && cp <= 2) entry = (uint32_t)(cp + 2);
+                }
+                sh.ntab[rk * 5 + (cc + 2)] = (uint8_t)entry;
+            }
+            lds_barrier();                                                   // 4
+            // 4. one wave composes the tables: correction after each near lane
+            if (wave == 0) {
+                uint32_t f = pack_ident();
+                if (lane < NN) {
+                    f = 0;
+                    for (int q = 0; q < 5; q++) f |= (uint32_t)sh.ntab[lane * 5 + q] << (3 * q);
+                }
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t g = __shfl_up(f, off, 64);
+                    if (lane >= (uint32_t)off) f = compose(f, g);
+                }
+                const uint32_t c0v = (f >> 6) & 7u;                          // entry for c = 0
+                const uint64_t smask = __ballot(lane < NN && c0v == STOPC);
+                if (lane < NN) sh.cafter[lane] = (int8_t)((int32_t)c0v - 2);
+                if (lane == 0) sh.stop_lane = smask ? sh.nlane[__ffsll((unsigned long long)smask) - 1] : (uint32_t)NC;
+            }
+            lds_barrier();                                                   // 5
+            if (sh.stop_lane < eidx) eidx = sh.stop_lane;
+            // 5. every lane up to e: the exact step from its true predecessor
+            bool bad = false;
+            TbEval v{};
+            int64_t Dexp = 0;
+            if (mine && tid <= eidx) {
+                const int32_t cin = nrank > 0 ? (int32_t)sh.cafter[nrank - 1] : 0;
+                v = tb_eval(mode, D + Pj + cin, E, P, R, alive, add, cap, nd, profile);
+                const int32_t cout = near ? (nrank < MAX_NEAR ? (int32_t)sh.cafter[nrank] : 99) : cin;
+                Dexp = D + Pj + r + cout;
+                if (tid < eidx) bad = !(alive && v.inrange && !v.allowed && !v.clamped && v.Dact == Dexp);
+            }
+            const uint64_t bmask = __ballot(bad);
+            if (!loader && lane == 0)
+                sh.wbad[wave] = bmask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bmask) - 1) : (uint32_t)NC;
+            lds_barrier();                                                   // 6
+            for (int w = 0; w < NWC; w++) eidx = sh.wbad[w] < eidx ? sh.wbad[w] : eidx;
+            // 6. commit lanes [first, e]; e's exact result is the next base
+            if (mine && tid <= eidx) write_out(a, i, tb_outputs(v, rq.n, rq.reset, cf.rate, cf.inv_rate));
+            if (tid == eidx) {
+                TbQ q = (v.inrange && mode == QM_DEC) || (v.inrange && mode == QM_BIN) ? TbQ{v.Dact, E}
+                                                                                     : tb_quant(v.tokens, profile);
                 sh.baseD = q.D;
                 sh.baseE = q.E;
             }
-            lds_barrier();                                               // C
-            RL_STAMP(t1);
-#ifdef RL_STAMPS
-            cyc[4] += t1 - t0;
-#endif
-            first = s + 1;
+            lds_barrier();                                                   // 7
+            first = eidx + 1;
         }
-        if (tid == cnt - 1) {
-            sh.carryL = Lq;
-            sh.carryW = wafter;
-        }
-        if (loader) {        // chunk k+1 (loaded during this chunk) -> ring; start chunk k+2
+        if (loader) {          // chunk k+1 -> ring, start loading chunk k+2
             st_fields((k + 1) & 1);
-            ld_fields(base + 2 * COOP);
+            ld_fields(base + 2 * NC);
         }
         lds_barrier();
     }
     if (tid == 0) {
         e->tok = tb_value(sh.baseD, sh.baseE, profile);
-        e->last = sh.carryL;
-        e->when = sh.carryW;
+        e->last = pre.lq[j1 - 1];
+        e->when = pre.when[j1 - 1];
         if (dbg) { atomicAdd(&dbg[0], nrounds); atomicAdd(&dbg[1], nchunks); }
-#ifdef RL_STAMPS
-        // phase cycles of the LONGEST cooperative segment of the batch (max)
-        if (dbg) for (int k = 0; k < 5; k++) atomicMax((unsigned long long*)&dbg[8 + 2 * k], (unsigned long long)cyc[k]);
-#endif
     }
 }
 
@@ -500,18 +654,46 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
 }
 
 // requests in sorted order (one coalesced pass; random reads of the 28 B
-// request records, which stay in the Infinity Cache at 1M-request batches)
+// request records, which stay in the Infinity Cache at 1M-request batches),
+// plus the token-bucket precomputation (TbPre)
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-                                                 uint32_t m, uint32_t invalid_key, ReqArgs in, ReqArgs out) {
+                                                 uint32_t m, uint32_t invalid_key, uint32_t win_base,
+                                                 const TbEntry* __restrict__ tb, const CfgDev* __restrict__ cfgs,
+                                                 int32_t profile, ReqArgs in, ReqArgs out, TbPre pre) {
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
-        if (sk[j] == invalid_key) continue;
-        uint32_t i = sv[j];
-        int64_t t = in.ts[i];
+        const uint32_t k0 = sk[j];
+        if (k0 == invalid_key) continue;
+        const uint32_t i = sv[j];
+        const int64_t t = in.ts[i];
+        const uint32_t c = in.cfg[i];
+        const int64_t sms = in.sms ? in.sms[i] : floor_div(t, 1000000LL);
         // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
         const_cast<int64_t*>(out.ts)[j] = t;
         const_cast<int64_t*>(out.n)[j] = in.n[i];
-        const_cast<uint32_t*>(out.cfg)[j] = in.cfg[i];
-        const_cast<int64_t*>(out.sms)[j] = in.sms ? in.sms[i] : floor_div(t, 1000000LL);
+        const_cast<uint32_t*>(out.cfg)[j] = c;
+        const_cast<int64_t*>(out.sms)[j] = sms;
+        if (k0 >= win_base) continue;
+        const CfgDev& C = cfgs[c];
+        const double now = (double)t / 1e9;
+        double prev_last;
+        int64_t prev_when;
+        if (j == 0 || sk[j - 1] != k0) {
+            prev_last = tb[k0].last;
+            prev_when = tb[k0].when;
+        } else {
+            const uint32_t ip = sv[j - 1];
+            const int64_t tp = in.ts[ip];
+            const int64_t smsp = in.sms ? in.sms[ip] : floor_div(tp, 1000000LL);
+            prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
+            prev_when = expire_when(cfgs[in.cfg[ip]].ttl_tb, smsp);
+        }
+        const bool alive = key_alive(prev_when, sms, profile);
+        const double last = alive ? prev_last : now;
+        pre.add[j] = (now - last) * C.rate;
+        pre.alive[j] = alive ? 1 : 0;
+        pre.reset[j] = tb_reset_at(now, C);
+        pre.lq[j] = lua_tostring_roundtrip(now, profile);
+        pre.when[j] = expire_when(C.ttl_tb, sms);
     }
 }
 
@@ -531,14 +713,17 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
 
 // Work-queue replay: blocks first drain the heavy list (one segment per block,
 // cooperative), then the light list (256 segments per grab, one per thread).
+constexpr int COOP_NC = 448;                 // compute lanes per cooperative block
+constexpr int REPLAY_BLOCK = COOP_NC + 64;  // + one loader wave
+
 template <bool LCFG>
 __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     const uint32_t* __restrict__ sk, const SegRec* __restrict__ heavy,
     const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
     const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
-    const CfgDev* __restrict__ gcfgs, uint32_t ncfg, int32_t profile, ReqArgs a, uint32_t* eflags,
+    const CfgDev* __restrict__ gcfgs, uint32_t ncfg, int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
     uint32_t* dbg) {
-    __shared__ CoopShared sh;
+    __shared__ CoopShared<COOP_NC> sh;
     __shared__ uint32_t s_u;
     __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
     if (LCFG) {
@@ -556,7 +741,7 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
         const SegRec sg = heavy[u];
         const uint32_t k0 = sk[sg.j0];
         if (k0 < win_base) {
-            replay_tb_coop(sh, &tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, dbg);
+            replay_tb_coop<COOP_NC>(sh, &tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, dbg);
         } else if (threadIdx.x == 0) {
             replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
@@ -572,7 +757,7 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
         if (u < nlight) {
             const SegRec sg = light[u];
             const uint32_t k0 = sk[sg.j0];
-            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a);
+            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre);
             else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
     }
