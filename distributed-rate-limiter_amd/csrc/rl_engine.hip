@@ -138,7 +138,7 @@ constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
 constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2,3] queue heads
 constexpr uint32_t CTRL_DBG = CTRL_NSEG + 4;   // [0] coop rounds [1] coop chunks [8..17] stamps
-constexpr uint32_t CTRL_WORDS = CTRL_DBG + 20;
+constexpr uint32_t CTRL_WORDS = CTRL_DBG + 24;
 
 uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1;
@@ -512,10 +512,11 @@ extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t 
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     if (!e || !out) return RL_EINVAL;
     (void)hipSetDevice(e->device);
-    uint32_t c[24] = {0};
+    uint32_t c[28] = {0};
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(c, e->d_ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 5; k++) e->stats.stamp_cycles[k] = ((uint64_t)c[4 + 8 + 2 * k + 1] << 32) | c[4 + 8 + 2 * k];
+    for (int k = 0; k < 6; k++) e->stats.stamp_cycles[k] = ((uint64_t)c[4 + 8 + 2 * k + 1] << 32) | c[4 + 8 + 2 * k];
+    e->stats.stamp_cycles[6] = c[4 + 2];   // max rounds of one segment
     e->stats.last_heavy = c[0];
     e->stats.last_segments = (uint64_t)c[0] + c[1];
     e->stats.last_coop_rounds = c[4];

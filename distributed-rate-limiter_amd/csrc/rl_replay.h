@@ -363,6 +363,31 @@ __device__ inline uint32_t compose(uint32_t f, uint32_t g) {
     return h;
 }
 
+// generic 32-bit wave64 inclusive scan with DPP; `op(self, earlier)`
+template <int CTRL, int RM>
+__device__ inline uint32_t dpp32(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, RM, 0xf, false);
+}
+template <typename Op>
+__device__ inline uint32_t wave_scan_u32(uint32_t v, uint32_t ident, Op op) {
+    v = op(v, dpp32<0x111, 0xf>(v, ident));
+    v = op(v, dpp32<0x112, 0xf>(v, ident));
+    v = op(v, dpp32<0x114, 0xf>(v, ident));
+    v = op(v, dpp32<0x118, 0xf>(v, ident));
+    v = op(v, dpp32<0x142, 0xa>(v, ident));
+    v = op(v, dpp32<0x143, 0xc>(v, ident));
+    return v;
+}
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+    v = wave_scan_u32(v, 0xffffffffu, [](uint32_t a, uint32_t b) { return a < b ? a : b; });
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ inline int64_t readlane_i64(int64_t v, uint32_t l) {
+    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), (int)l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 template <int NC>
 struct CoopShared {
     ChunkSlot ring[2][NC];            // chunk k in slot k&1, filled by the loader wave
@@ -390,6 +415,13 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
     const bool loader = wave == (uint32_t)NWC;
     const uint64_t lt = (1ull << lane) - 1ull;
     uint32_t nrounds = 0, nchunks = 0;
+    uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, t1 = 0;
+    (void)cyc; (void)t0; (void)t1;
+#ifdef RL_STAMPS
+#define RL_PHASE(k) do { RL_STAMP(t1); cyc[k] += t1 - t0; t0 = t1; } while (0)
+#else
+#define RL_PHASE(k) do { } while (0)
+#endif
     if (tid == 0) {
         TbQ q = tb_quant(e->tok, profile);
         sh.baseD = q.D;
@@ -433,6 +465,7 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
         const bool alive = rq.alive != 0;
         nchunks++;
         uint32_t first = 0;
+        RL_STAMP(t0);
         while (first < cnt) {              // block-uniform
             nrounds++;
             const int64_t D = sh.baseD;
@@ -488,12 +521,16 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
                 if (lane == 0) sh.wnear[wave] = nmask;
             }
             lds_barrier();                                                   // 1
-            int64_t pre_sum = 0;
-            uint32_t nbefore = 0;
-            for (uint32_t w = 0; w < wave && w < (uint32_t)NWC; w++) {
-                pre_sum += sh.wtot[w];
-                nbefore += (uint32_t)__popcll(sh.wnear[w]);
-            }
+            RL_PHASE(0);
+            // cross-wave prefixes: one LDS read per lane, DPP scans, readlane
+            const int64_t wt = lane < (uint32_t)NWC ? sh.wtot[lane] : 0;
+            const uint64_t wn = lane < (uint32_t)NWC ? sh.wnear[lane] : 0ull;
+            const uint32_t wnc = (uint32_t)__popcll(wn);
+            const int64_t wt_inc = wave_incl_scan_i64(wt);
+            const uint32_t wn_inc = wave_scan_u32(wnc, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+            const uint32_t wsel = wave < (uint32_t)NWC ? wave : 0u;
+            const int64_t pre_sum = wave < (uint32_t)NWC ? readlane_i64(wt_inc - wt, wsel) : 0;
+            const uint32_t nbefore = wave < (uint32_t)NWC ? (uint32_t)__builtin_amdgcn_readlane((int)(wn_inc - wnc), (int)wsel) : 0u;
             const int64_t Pj = pre_sum + inc - rin;                          // exclusive prefix
             const uint32_t nrank = nbefore + (loader ? 0u : (uint32_t)__popcll(nmask & lt));
             // 2. events possible even with |c| <= 2
@@ -509,15 +546,16 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
             if (!loader && lane == 0)
                 sh.wev[wave] = emask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)emask) - 1) : (uint32_t)NC;
             lds_barrier();                                                   // 2
-            uint32_t eidx = NC;
-            for (int w = 0; w < NWC; w++) eidx = sh.wev[w] < eidx ? sh.wev[w] : eidx;
+            uint32_t eidx = wave_min_u32(lane < (uint32_t)NWC ? sh.wev[lane] : (uint32_t)NC);
             if (eidx >= cnt) eidx = cnt - 1;
             // near-tie lanes strictly before e: publish their inputs
             uint32_t NN = 0;
             {
                 const uint32_t ew = eidx >> 6, el = eidx & 63;
-                for (uint32_t w = 0; w < ew; w++) NN += (uint32_t)__popcll(sh.wnear[w]);
-                NN += (uint32_t)__popcll(sh.wnear[ew] & ((1ull << el) - 1ull));
+                const uint32_t before = (uint32_t)__builtin_amdgcn_readlane((int)(wn_inc - wnc), (int)ew);
+                const uint64_t wmask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wn, (int)ew) |
+                                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wn >> 32), (int)ew) << 32);
+                NN = before + (uint32_t)__popcll(wmask & ((1ull << el) - 1ull));
             }
             if (mine && near && tid < eidx) {
                 sh.nadd[nrank] = add;
@@ -528,6 +566,7 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
                 sh.nlane[nrank] = tid;
             }
             lds_barrier();                                                   // 3
+            RL_PHASE(1);
             // 3. candidate tables: one (near lane, c) pair per compute thread
             if (!loader && tid < NN * 5) {
                 const uint32_t rk = tid / 5;
@@ -543,6 +582,7 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
                 sh.ntab[rk * 5 + (cc + 2)] = (uint8_t)entry;
             }
             lds_barrier();                                                   // 4
+            RL_PHASE(2);
             // 4. one wave composes the tables: correction after each near lane
             if (wave == 0) {
                 uint32_t f = pack_ident();
@@ -550,17 +590,14 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
                     f = 0;
                     for (int q = 0; q < 5; q++) f |= (uint32_t)sh.ntab[lane * 5 + q] << (3 * q);
                 }
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t g = __shfl_up(f, off, 64);
-                    if (lane >= (uint32_t)off) f = compose(f, g);
-                }
+                f = wave_scan_u32(f, pack_ident(), [](uint32_t x, uint32_t y) { return compose(x, y); });
                 const uint32_t c0v = (f >> 6) & 7u;                          // entry for c = 0
                 const uint64_t smask = __ballot(lane < NN && c0v == STOPC);
                 if (lane < NN) sh.cafter[lane] = (int8_t)((int32_t)c0v - 2);
                 if (lane == 0) sh.stop_lane = smask ? sh.nlane[__ffsll((unsigned long long)smask) - 1] : (uint32_t)NC;
             }
             lds_barrier();                                                   // 5
+            RL_PHASE(3);
             if (sh.stop_lane < eidx) eidx = sh.stop_lane;
             // 5. every lane up to e: the exact step from its true predecessor
             bool bad = false;
@@ -577,7 +614,11 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
             if (!loader && lane == 0)
                 sh.wbad[wave] = bmask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bmask) - 1) : (uint32_t)NC;
             lds_barrier();                                                   // 6
-            for (int w = 0; w < NWC; w++) eidx = sh.wbad[w] < eidx ? sh.wbad[w] : eidx;
+            RL_PHASE(4);
+            {
+                const uint32_t mb = wave_min_u32(lane < (uint32_t)NWC ? sh.wbad[lane] : (uint32_t)NC);
+                eidx = mb < eidx ? mb : eidx;
+            }
             // 6. commit lanes [first, e]; e's exact result is the next base
             if (mine && tid <= eidx) write_out(a, i, tb_outputs(v, rq.n, rq.reset, cf.rate, cf.inv_rate));
             if (tid == eidx) {
@@ -587,6 +628,7 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
                 sh.baseE = q.E;
             }
             lds_barrier();                                                   // 7
+            RL_PHASE(5);
             first = eidx + 1;
         }
         if (loader) {          // chunk k+1 -> ring, start loading chunk k+2
@@ -600,6 +642,12 @@ __device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j
         e->last = pre.lq[j1 - 1];
         e->when = pre.when[j1 - 1];
         if (dbg) { atomicAdd(&dbg[0], nrounds); atomicAdd(&dbg[1], nchunks); }
+#ifdef RL_STAMPS
+        if (dbg) {
+            atomicMax(&dbg[2], nrounds);
+            for (int q = 0; q < 6; q++) atomicMax((unsigned long long*)&dbg[8 + 2 * q], (unsigned long long)cyc[q]);
+        }
+#endif
     }
 }
 

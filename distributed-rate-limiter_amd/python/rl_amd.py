@@ -57,7 +57,7 @@ class rl_stats(C.Structure):
         ("last_coop_chunks", C.c_uint64),
         ("sort_bits", C.c_uint32),
         ("sort_passes", C.c_uint32),
-        ("stamp_cycles", C.c_uint64 * 5),
+        ("stamp_cycles", C.c_uint64 * 7),
     ]
 
 

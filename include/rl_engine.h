@@ -73,7 +73,7 @@ typedef struct rl_stats {
     uint64_t last_coop_chunks; /* 256-request chunks of the last batch's heavy segments */
     uint32_t sort_bits;
     uint32_t sort_passes;
-    uint64_t stamp_cycles[5];  /* diagnostic build only: coop phase cycles (load, scan, eval, vote, commit) */
+    uint64_t stamp_cycles[7];  /* diagnostic build only: coop phase cycles of the longest segment, [6] = its rounds */
 } rl_stats;
 
 /* replaces redis.NewClient + NewTokenBucket/NewSlidingWindow/NewFixedWindow's
