@@ -43,6 +43,10 @@ def make_workload(name, batch, rank):
         return traces.SlidingWindowBursty(batch=batch, seed=4 + 1000 * rank)
     if name == "mixed":
         return traces.MixedTenants(batch=batch, seed=5 + 1000 * rank)
+    if name == "tb_zipf15":
+        return traces.TokenBucketZipf(batch=batch, s=1.5, seed=3 + 1000 * rank)
+    if name == "tb_hot":
+        return traces.TokenBucketZipf(nkeys=1, batch=batch, seed=3 + 1000 * rank)
     raise SystemExit(f"unknown workload {name}")
 
 
@@ -51,6 +55,8 @@ WORKLOAD_DESC = {
     "fw_uniform": "configs[0]: Fixed Window 100/min, 10k uniform keys",
     "sw_bursty": "configs[2]: Sliding Window 100/min, 100M keys, uniform + bursty",
     "mixed": "configs[3]: mixed TB/SW/FW by key mod 3, 1B keys uniform",
+    "tb_zipf15": "configs[4] key mix: Token Bucket 20/12s, 1M keys Zipf s=1.5 (top key 38%), batch 1M",
+    "tb_hot": "diagnostic: Token Bucket 20/12s, one key, batch 1M",
 }
 
 
@@ -116,7 +122,8 @@ def main():
 
     algs = {a for a, _, _ in gen.configs}
     need_tb = 1 in algs
-    keyspace = {"tb_zipf": 1 << 21, "fw_uniform": 1 << 15, "sw_bursty": 1 << 27, "mixed": 1 << 26}[args.workload]
+    keyspace = {"tb_zipf": 1 << 21, "tb_zipf15": 1 << 21, "tb_hot": 1 << 10, "fw_uniform": 1 << 15,
+                "sw_bursty": 1 << 27, "mixed": 1 << 26}[args.workload]
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7,
                         tb_capacity=keyspace if need_tb else 1024,
                         win_capacity=keyspace if algs - {1} else 1024,
@@ -200,7 +207,8 @@ def main():
                      "bytes_per_decision": bytes_per_dec},
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
-                          "coop_rounds": int(st.last_coop_rounds), "coop_chunks": int(st.last_coop_chunks)},
+                          "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
+                          "coop_ends": [int(x) for x in st.coop_ends]},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
                                                     (stage_ms / nbat).tolist())},
     }

@@ -182,8 +182,9 @@ struct rl_engine {
     double* o_tok = nullptr;
     // token-bucket precomputation (k_permute)
     double *q_add = nullptr, *q_lq = nullptr;
-    int64_t *q_reset = nullptr, *q_when = nullptr;
-    uint8_t* q_alive = nullptr;
+    uint64_t* q_nc = nullptr;
+    TbRuns runs{};            // cooperative replay's committed runs (by start position)
+    int64_t* q_when = nullptr;
     SegRec* d_light = nullptr;
     int replay_grid = 2048;
     uint32_t heavy_min = 32;   // segments this long replay cooperatively
@@ -232,8 +233,8 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->p_ts); (void)hipFree(e->p_n); (void)hipFree(e->p_sms); (void)hipFree(e->p_cfg);
     (void)hipFree(e->o_dec); (void)hipFree(e->o_rem); (void)hipFree(e->o_retry); (void)hipFree(e->o_reset);
     (void)hipFree(e->o_tok);
-    (void)hipFree(e->q_add); (void)hipFree(e->q_lq); (void)hipFree(e->q_reset); (void)hipFree(e->q_when);
-    (void)hipFree(e->q_alive);
+    (void)hipFree(e->q_add); (void)hipFree(e->q_nc);
+    (void)hipFree(e->runs.len); (void)hipFree(e->runs.E); (void)hipFree(e->runs.D0); (void)hipFree(e->runs.D1); (void)hipFree(e->q_lq); (void)hipFree(e->q_when);
     (void)hipFree(e->d_light);
     (void)hipFree(e->d_zero);
     (void)hipFree(e->d_eflags);
@@ -265,6 +266,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
     size_t M = e->max_batch;
+    // q_add and q_nc carry 4 elements of slack: the replay's loader wave reads
+    // them in aligned 16-byte pairs that may end past the last request
     e->cfg_cap = 64;
     bool ok = true;
     ok &= hipMalloc(&e->d_cfg, sizeof(CfgDev) * e->cfg_cap) == hipSuccess;
@@ -284,11 +287,14 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->o_retry, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_tok, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_add, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->q_add, 8 * (M + 4)) == hipSuccess;
+    ok &= hipMalloc(&e->q_nc, 8 * (M + 4)) == hipSuccess;
+    ok &= hipMalloc(&e->runs.len, 2 * M) == hipSuccess;
+    ok &= hipMalloc(&e->runs.E, 2 * M) == hipSuccess;
+    ok &= hipMalloc(&e->runs.D0, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&e->runs.D1, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->q_lq, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->q_when, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_alive, M) == hipSuccess;
     ok &= hipMalloc(&e->d_light, sizeof(SegRec) * M) == hipSuccess;
     e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
     ok &= hipMalloc(&e->d_zero, e->zero_bytes) == hipSuccess;
@@ -309,6 +315,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     k_init_tb<<<2048, 256, 0, e->stream>>>(e->d_tb, e->tb_cap);
     k_init_win<<<2048, 256, 0, e->stream>>>(e->d_win, e->win_cap);
     if (hipMemsetAsync(e->d_eflags, 0, 4, e->stream) != hipSuccess) return bail(RL_EDEVICE);
+    // run lengths start at 0; k_tb_expand clears every one it consumes
+    if (hipMemsetAsync(e->runs.len, 0, 2 * M, e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_REPLAY_GRID")) e->replay_grid = atoi(v);
@@ -401,10 +409,12 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
     k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->heavy_min, e->d_heavy, segctr, e->d_light,
                                       segctr + 1);
-    ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset,
-               a.tok ? e->o_tok : nullptr};
+    // sorted-order buffers; tokens always kept (token-bucket results derive from them)
+    ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset, e->o_tok};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
-    TbPre pre{e->q_add, e->q_reset, e->q_lq, e->q_when, e->q_alive};
+    // the TB reset time is state-independent: k_permute writes it straight
+    // into the sorted result buffer
+    TbPre pre{e->q_add, e->q_nc, e->o_reset, e->q_lq, e->q_when};
     k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_tb, e->d_cfg, e->profile, a, ps,
                                     pre);
     if (e->timing) (void)hipEventRecord(ev[3], s);
@@ -413,13 +423,14 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
         k_replay<true><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                               segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
                                                               ncfg, e->profile, ps, pre, e->d_eflags,
-                                                              e->d_ctrl + CTRL_DBG);
+                                                              e->d_ctrl + CTRL_DBG, e->runs);
     else
         k_replay<false><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                                segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
                                                                ncfg, e->profile, ps, pre, e->d_eflags,
-                                                              e->d_ctrl + CTRL_DBG);
-    k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, ps, a);
+                                                              e->d_ctrl + CTRL_DBG, e->runs);
+    k_tb_expand<<<pgrid, 256, 0, s>>>(m, e->runs, e->d_cfg, e->profile, ps, pre, e->d_eflags);
+    k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     if (e->timing) {
         (void)hipEventRecord(ev[4], s);
         e->ev_pending.push_back(ev);
@@ -434,6 +445,7 @@ static int check_flags(rl_engine* e, uint32_t f) {
     if (f & EF_TABLE_FULL) return fail(e, RL_ENOMEM, "state table full");
     if (f & EF_LOOKBACK) return fail(e, RL_ETIMEOUT, "radix sort look-back timed out");
     if (f & EF_ORDER) return fail(e, RL_EORDER, "per-key window ids went backwards");
+    if (f & EF_INTERNAL) return fail(e, RL_EDEVICE, "cooperative replay invariant violated");
     return RL_OK;
 }
 
@@ -520,7 +532,8 @@ extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     e->stats.last_heavy = c[0];
     e->stats.last_segments = (uint64_t)c[0] + c[1];
     e->stats.last_coop_rounds = c[4];
-    e->stats.last_coop_chunks = c[5];
+    e->stats.last_coop_iters = c[5];
+    for (int k = 0; k < 4; k++) e->stats.coop_ends[k] = c[4 + 3 + k];   // dbg[3..6]
     *out = e->stats;
     return RL_OK;
 }

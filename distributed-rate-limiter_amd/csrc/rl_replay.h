@@ -32,11 +32,14 @@ struct ReqArgs {
 // computed in the permute pass: the previous request of the same key is the
 // previous sorted position (or, for a segment head, the table entry).
 struct TbPre {
-    double* add;       // elapsed * refill_rate (tokenbucket.go:36-37)
-    int64_t* reset;    // calculateResetTime (tokenbucket.go:161-165)
+    double* add;       // elapsed * refill_rate (tokenbucket.go:36-37); NaN when HMGET finds
+                       // no live key (tokenbucket.go:31-34: tokens = capacity, add = 0)
+    uint64_t* nc;      // (cfg << 32) | n for the cooperative replay's loader; n field 0
+                       // when n >= 2^31 (the exact path then reads ReqArgs::n)
+    int64_t* reset;    // calculateResetTime (tokenbucket.go:161-165); aliases the sorted
+                       // result buffer, so TB replay never rewrites reset_at
     double* lq;        // tostring(now) as stored in last_refill (tokenbucket.go:48)
     int64_t* when;     // key expiry after this request's EXPIRE (tokenbucket.go:49)
-    uint8_t* alive;    // did HMGET see the key (tokenbucket.go:31-33)
 };
 
 __device__ inline int64_t req_server_ms(const ReqArgs& a, uint32_t i, int64_t t) {
@@ -49,6 +52,15 @@ __device__ inline void write_out(const ReqArgs& a, uint32_t i, const Out& o) {
     a.retry[i] = o.retry;
     a.reset[i] = o.reset_at;
     if (a.tok) a.tok[i] = o.tokens;
+}
+
+// token bucket: replay writes the decision and the unquantized tokens only;
+// reset_at was written by k_permute (TbPre::reset) and remaining/retry_after
+// are functions of (decision, tokens, n, config) that k_unpermute evaluates
+// (tokenbucket.go:114-130, tb_result below)
+__device__ inline void write_out_tb(const ReqArgs& a, uint32_t i, uint8_t dec, double tokens) {
+    a.dec[i] = dec;
+    a.tok[i] = tokens;
 }
 
 // end of the run of `k0` starting at j0 in the sorted keys (galloping search)
@@ -112,8 +124,10 @@ __device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, co
                                         int32_t profile, const ReqArgs& a, const TbPre& pre) {
     double tok = e->tok;
     for (uint32_t j = j0; j < j1; j++) {
-        Out o = tb_chain_step(tok, pre.alive[j] != 0, pre.add[j], a.n[j], pre.reset[j], cfgs[a.cfg[j]], profile);
-        write_out(a, j, o);
+        const double add = pre.add[j];
+        const bool alive = add == add;
+        Out o = tb_chain_step(tok, alive, alive ? add : 0.0, a.n[j], 0, cfgs[a.cfg[j]], profile);
+        write_out_tb(a, j, o.decision, o.tokens);
     }
     e->tok = tok;
     e->last = pre.lq[j1 - 1];
@@ -141,30 +155,6 @@ __device__ inline void replay_win_serial(WinEntry* e, uint32_t j0, uint32_t j1, 
     if (ef) atomicOr(eflags, ef);
 }
 
-// ---------------------------------------------------------------------------
-// Block-cooperative token-bucket replay for heavy (Zipf hot-key) segments.
-//
-// The carried state of a token-bucket key is the *stored* tokens value, which
-// Lua's tostring quantizes: in Redis 7 to 14 significant decimal digits, i.e.
-// an integer D in [1e13, 1e14) and a decade E (value = D * 10^(E-13)); with
-// miniredis to the exact double, i.e. an integer mantissa D and binary
-// exponent E.  Between events a step's effect on D is the state-independent
-// increment r_j = round(add_j * 10^(13-E)) (resp. add_j * 2^-E), because D is
-// an integer and only the rounding of the fractional part of add_j matters.
-//
-// Guess-and-verify, one round per pass over the not-yet-committed lanes:
-//   1. each lane computes its nominal r_j (state-independent),
-//   2. block exclusive scan: guessed predecessor state Dg_j = D + sum r_<j,
-//   3. each lane runs the reference step EXACTLY (tb_step's arithmetic) from
-//      the guess and checks its exact result equals (Dg_j + r_j, E),
-//   4. the first lane s that does not (a near-tie rounding flip, a decade
-//      change, an allow, a clamp at capacity, an expired key) had a correct
-//      guess -- every lane before it was verified -- so lanes <= s are
-//      committed and s's exact result is the new base.
-// The result is identical to serial replay by construction; the common case
-// (denied requests accumulating refill) commits 256 steps per round.
-// ---------------------------------------------------------------------------
-
 struct TbQ {
     int64_t D;
     int32_t E;
@@ -191,17 +181,6 @@ __device__ inline double tb_value(int64_t D, int32_t E, int32_t profile) {
         return D < 0 ? -v : v;
     }
     return ldexp((double)D, E);
-}
-
-// 1 / (unit of D) for decade/exponent E (only used for the nominal guess)
-__device__ inline double tb_scale(int32_t E, int32_t profile) {
-    if (profile != PROFILE_REDIS7) return ldexp(1.0, -E);
-    int k = 13 - E;
-    int ak = k < 0 ? -k : k;
-    double s = 1.0;
-    while (ak > 22) { s *= 1e22; ak -= 22; }
-    s *= rlq::pow10_exact(ak);
-    return k >= 0 ? s : 1.0 / s;
 }
 
 // Diagnostic build only (-DRL_STAMPS): per-phase shader-clock sums of the
@@ -243,47 +222,8 @@ __device__ inline int64_t wave_incl_scan_i64(int64_t v) {
     return v;
 }
 
-// ---------------------------------------------------------------------------
-// In-round flip resolution.
-//
-// Within a decade (Redis profile) or binade (miniredis profile) the stored
-// state is an integer D, and a step maps D to D + r_j, r_j = round(add_j / u),
-// except when add_j / u lies within TAU of a half-integer: then the IEEE
-// rounding of T = strtod(D) and of T + add (|error| <= 0.0222 u, SURVEY-level
-// bound 10^14 * 2^-52) can flip the rounded result by one.  So a lane whose
-// fraction is far from 1/2 maps a predecessor error c to the same c; only
-// near-tie lanes depend on the exact predecessor.  One round:
-//   1. nominal r_j, near-tie flag; block scan of r (DPP) -> nominal
-//      predecessor D + P_j; compaction rank of the near-tie lanes,
-//   2. first lane e where an event (allow, clamp, decade change, expired key,
-//      > 64 near lanes) is possible even with |c| <= 2,
-//   3. every near-tie lane before e is evaluated EXACTLY for the five
-//      candidate predecessors D + P_j + c, c in [-2, 2] (one (lane, c) pair
-//      per thread): a table c -> c' (or STOP),
-//   4. one wave composes the tables (a function-composition scan) -> the true
-//      correction after each near-tie lane; a STOP shortens the round,
-//   5. every lane up to e runs the step EXACTLY from its now-known true
-//      predecessor and checks the result it implies; the first mismatch (none
-//      if the bound holds) also ends the round -- correctness never rests on
-//      the bound, only the speed does,
-//   6. lanes up to e are committed; e's exact result is the next base.
-// Rounds per chunk = 1 + events, not 1 + flips.
-// ---------------------------------------------------------------------------
-
-// One chunk's requests as the loader wave hands them to the compute waves
-// (state-independent terms precomputed by k_permute).
-struct ChunkSlot {
-    double add;
-    int64_t n;
-    int64_t reset;
-    uint32_t c;
-    uint32_t alive;
-};
-
 // configs cached in LDS per block (when the engine has at most MAX_LCFG)
 constexpr int MAX_LCFG = 32;
-constexpr int MAX_NEAR = 64;
-constexpr uint32_t STOPC = 7;
 constexpr double TAU_DEC = 0.03;   // > 0.0222: far lanes are exact by the bound
 
 enum : int { QM_NONE = 0, QM_DEC = 1, QM_BIN = 2 };
@@ -302,7 +242,10 @@ __device__ inline TbEval tb_eval(int mode, int64_t Dpred, int32_t E, double P, d
     TbEval v;
     double T;
     if (!alive) T = cap;
-    else if (mode == QM_DEC) T = rlq::div_pow10((double)Dpred, P, R);   // strtod("D e(E-13)")
+    else if (mode == QM_DEC) {                                           // strtod("D e(E-13)")
+        const double t = rlq::div_pow10((double)(Dpred < 0 ? -Dpred : Dpred), P, R);
+        T = Dpred < 0 ? -t : t;
+    }
     else if (mode == QM_BIN) T = (double)Dpred * R;                      // exact: R = 2^E
     else T = tb_value(Dpred, E, profile);
     const double sum = T + add;
@@ -313,18 +256,20 @@ __device__ inline TbEval tb_eval(int mode, int64_t Dpred, int32_t E, double P, d
     v.tokens = tokens;
     v.Dact = 0;
     v.inrange = false;
+    const double at = tokens < 0.0 ? -tokens : tokens;                   // %.14g is sign-symmetric
     if (mode == QM_DEC) {
-        if (tokens > 0.0 && tokens * P < 1.4e14) {
-            v.Dact = rlq::round_scaled_P(tokens, P);
+        if (at > 0.0 && at * P < 1.4e14) {
+            v.Dact = rlq::round_scaled_P(at, P);
             v.inrange = v.Dact >= 10000000000000LL && v.Dact < 100000000000000LL;
         }
     } else if (mode == QM_BIN) {
-        const double w = tokens * P;                                     // exact scaling
+        const double w = at * P;                                         // exact scaling
         if (w >= 4503599627370496.0 && w < 9007199254740992.0) {
             v.Dact = (int64_t)w;
             v.inrange = (double)v.Dact == w;
         }
     }
+    if (tokens < 0.0) v.Dact = -v.Dact;
     return v;
 }
 
@@ -344,23 +289,6 @@ __device__ inline Out tb_outputs(const TbEval& v, int64_t nn, int64_t reset_at, 
         o.retry = d < 0 ? 0 : d;
     }
     return o;
-}
-
-__device__ inline uint32_t pack_ident() {   // identity table: c -> c
-    uint32_t f = 0;
-    for (int k = 0; k < 5; k++) f |= (uint32_t)k << (3 * k);
-    return f;
-}
-// (f after g): apply g first, then f
-__device__ inline uint32_t compose(uint32_t f, uint32_t g) {
-    uint32_t h = 0;
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        uint32_t gk = (g >> (3 * k)) & 7u;
-        uint32_t hk = gk == STOPC ? STOPC : ((f >> (3 * gk)) & 7u);
-        h |= hk << (3 * k);
-    }
-    return h;
 }
 
 // generic 32-bit wave64 inclusive scan with DPP; `op(self, earlier)`
@@ -388,268 +316,11 @@ __device__ inline int64_t readlane_i64(int64_t v, uint32_t l) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
-template <int NC>
-struct CoopShared {
-    ChunkSlot ring[2][NC];            // chunk k in slot k&1, filled by the loader wave
-    int64_t wtot[NC / 64];
-    uint64_t wnear[NC / 64];
-    uint32_t wev[NC / 64];
-    uint32_t wbad[NC / 64];
-    double nadd[MAX_NEAR], ncap[MAX_NEAR], nnd[MAX_NEAR];
-    int64_t npred[MAX_NEAR], nr[MAX_NEAR];
-    uint32_t nlane[MAX_NEAR];
-    uint8_t ntab[MAX_NEAR * 5];
-    int8_t cafter[MAX_NEAR];
-    uint32_t stop_lane;
-    int64_t baseD;
-    int32_t baseE;
-};
+}  // namespace rl
 
-template <int NC>
-__device__ inline void replay_tb_coop(CoopShared<NC>& sh, TbEntry* e, uint32_t j0, uint32_t j1,
-                                      const CfgDev* __restrict__ cfgs, int32_t profile, const ReqArgs& a,
-                                      const TbPre& pre, uint32_t* dbg) {
-    constexpr int NWC = NC / 64;                 // compute waves
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63, wave = tid >> 6;
-    const bool loader = wave == (uint32_t)NWC;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t nrounds = 0, nchunks = 0;
-    uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t0 = 0, t1 = 0;
-    (void)cyc; (void)t0; (void)t1;
-#ifdef RL_STAMPS
-#define RL_PHASE(k) do { RL_STAMP(t1); cyc[k] += t1 - t0; t0 = t1; } while (0)
-#else
-#define RL_PHASE(k) do { } while (0)
-#endif
-    if (tid == 0) {
-        TbQ q = tb_quant(e->tok, profile);
-        sh.baseD = q.D;
-        sh.baseE = q.E;
-    }
-    // loader: the chunk after next, NC/64 entries per loader lane
-    ChunkSlot fld[NWC];
-    auto ld_fields = [&](uint32_t base) {
-#pragma unroll
-        for (int q = 0; q < NWC; q++) {
-            const uint32_t j = base + lane + 64 * q;
-            ChunkSlot f{0.0, 1, 0, 0, 0};
-            if (base < j1 && j < j1) {
-                f.add = pre.add[j];
-                f.n = a.n[j];
-                f.reset = pre.reset[j];
-                f.c = a.cfg[j];
-                f.alive = pre.alive[j];
-            }
-            fld[q] = f;
-        }
-    };
-    auto st_fields = [&](int slot) {
-#pragma unroll
-        for (int q = 0; q < NWC; q++) sh.ring[slot][lane + 64 * q] = fld[q];
-    };
-    if (loader) {
-        ld_fields(j0);
-        st_fields(0);
-        ld_fields(j0 + NC);
-    }
-    __syncthreads();
-    uint32_t k = 0;
-    for (uint32_t base = j0; base < j1; base += NC, k++) {
-        const uint32_t cnt = (j1 - base) < (uint32_t)NC ? (j1 - base) : (uint32_t)NC;
-        const bool act = !loader && tid < cnt;
-        const ChunkSlot rq = loader ? ChunkSlot{0.0, 1, 0, 0, 0} : sh.ring[k & 1][tid];
-        const uint32_t i = base + tid;     // sorted position
-        const CfgDev& cf = cfgs[rq.c];     // LDS copy (see k_replay)
-        const double add = rq.add, cap = cf.limit_d, nd = (double)rq.n;
-        const bool alive = rq.alive != 0;
-        nchunks++;
-        uint32_t first = 0;
-        RL_STAMP(t0);
-        while (first < cnt) {              // block-uniform
-            nrounds++;
-            const int64_t D = sh.baseD;
-            const int32_t E = sh.baseE;
-            int mode = QM_NONE;
-            double P = 1.0, R = 1.0, tau = 0.0;
-            if (profile == PROFILE_REDIS7) {
-                if (13 - E >= 1 && 13 - E <= 22 && D >= 10000000000000LL && D < 100000000000000LL) {
-                    mode = QM_DEC;
-                    P = rlq::pow10_exact(13 - E);
-                    R = 1.0 / P;
-                    tau = TAU_DEC;
-                }
-            } else if (D >= (1LL << 52) && D < (1LL << 53) && E > -1000 && E < 900) {
-                mode = QM_BIN;
-                P = ldexp(1.0, -E);
-                R = ldexp(1.0, E);
-            }
-            const bool mine = act && tid >= first;
-            if (mode == QM_NONE) {
-                // off the fast decades (or an empty/zero state): one exact step
-                if (tid == first) {
-                    TbEval v = tb_eval(QM_NONE, D, E, P, R, alive, add, cap, nd, profile);
-                    write_out(a, i, tb_outputs(v, rq.n, rq.reset, cf.rate, cf.inv_rate));
-                    TbQ q = tb_quant(v.tokens, profile);
-                    sh.baseD = q.D;
-                    sh.baseE = q.E;
-                }
-                lds_barrier();
-                first++;
-                continue;
-            }
-            // 1. nominal increment, near-tie flag, event flags that need no prefix
-            int64_t r = 0;
-            bool near = false, ev = !alive;
-            if (mine) {
-                const double pr = add * P;
-                const double err = (mode == QM_DEC) ? __builtin_fma(add, P, -pr) : 0.0;
-                const double rr = rint(pr);
-                if (!(pr < 1e15 && pr > -1e15)) {
-                    ev = true;
-                } else {
-                    r = (int64_t)rr;
-                    const double dist = fabs((pr - rr) + err);       // distance to nearest integer
-                    near = (mode == QM_DEC) ? dist > 0.5 - tau : dist >= 0.5;
-                }
-            }
-            const int64_t rin = mine ? r : 0;
-            const int64_t inc = wave_incl_scan_i64(rin);
-            const uint64_t nmask = __ballot(mine && near);
-            if (!loader) {
-                if (lane == 63) sh.wtot[wave] = inc;
-                if (lane == 0) sh.wnear[wave] = nmask;
-            }
-            lds_barrier();                                                   // 1
-            RL_PHASE(0);
-            // cross-wave prefixes: one LDS read per lane, DPP scans, readlane
-            const int64_t wt = lane < (uint32_t)NWC ? sh.wtot[lane] : 0;
-            const uint64_t wn = lane < (uint32_t)NWC ? sh.wnear[lane] : 0ull;
-            const uint32_t wnc = (uint32_t)__popcll(wn);
-            const int64_t wt_inc = wave_incl_scan_i64(wt);
-            const uint32_t wn_inc = wave_scan_u32(wnc, 0u, [](uint32_t x, uint32_t y) { return x + y; });
-            const uint32_t wsel = wave < (uint32_t)NWC ? wave : 0u;
-            const int64_t pre_sum = wave < (uint32_t)NWC ? readlane_i64(wt_inc - wt, wsel) : 0;
-            const uint32_t nbefore = wave < (uint32_t)NWC ? (uint32_t)__builtin_amdgcn_readlane((int)(wn_inc - wnc), (int)wsel) : 0u;
-            const int64_t Pj = pre_sum + inc - rin;                          // exclusive prefix
-            const uint32_t nrank = nbefore + (loader ? 0u : (uint32_t)__popcll(nmask & lt));
-            // 2. events possible even with |c| <= 2
-            if (mine && !ev) {
-                const int64_t Dn = D + Pj + r;
-                const int64_t M = 4;
-                if (mode == QM_DEC) ev = (Dn - M < 10000000000000LL) || (Dn + M >= 100000000000000LL);
-                else ev = (Dn - M < (1LL << 52)) || (Dn + M >= (1LL << 53));
-                const double vhi = (double)(Dn + M) * R * (1.0 + 1e-9);
-                ev = ev || vhi >= nd || vhi >= cap || (near && nrank >= (uint32_t)MAX_NEAR);
-            }
-            const uint64_t emask = __ballot(mine && ev);
-            if (!loader && lane == 0)
-                sh.wev[wave] = emask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)emask) - 1) : (uint32_t)NC;
-            lds_barrier();                                                   // 2
-            uint32_t eidx = wave_min_u32(lane < (uint32_t)NWC ? sh.wev[lane] : (uint32_t)NC);
-            if (eidx >= cnt) eidx = cnt - 1;
-            // near-tie lanes strictly before e: publish their inputs
-            uint32_t NN = 0;
-            {
-                const uint32_t ew = eidx >> 6, el = eidx & 63;
-                const uint32_t before = (uint32_t)__builtin_amdgcn_readlane((int)(wn_inc - wnc), (int)ew);
-                const uint64_t wmask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wn, (int)ew) |
-                                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wn >> 32), (int)ew) << 32);
-                NN = before + (uint32_t)__popcll(wmask & ((1ull << el) - 1ull));
-            }
-            if (mine && near && tid < eidx) {
-                sh.nadd[nrank] = add;
-                sh.ncap[nrank] = cap;
-                sh.nnd[nrank] = nd;
-                sh.npred[nrank] = D + Pj;
-                sh.nr[nrank] = r;
-                sh.nlane[nrank] = tid;
-            }
-            lds_barrier();                                                   // 3
-            RL_PHASE(1);
-            // 3. candidate tables: one (near lane, c) pair per compute thread
-            if (!loader && tid < NN * 5) {
-                const uint32_t rk = tid / 5;
-                const int32_t cc = (int32_t)(tid % 5) - 2;
-                const int64_t base_pred = sh.npred[rk];
-                TbEval v = tb_eval(mode, base_pred + cc, E, P, R, true, sh.nadd[rk], sh.ncap[rk], sh.nnd[rk],
-                                   profile);
-                uint32_t entry = STOPC;
-                if (v.inrange && !v.allowed && !v.clamped) {
-                    const int64_t cp = v.Dact - (base_pred + sh.nr[rk]);
-                    if (cp >= -2 && cp <= 2) entry = (uint32_t)(cp + 2);
-                }
-                sh.ntab[rk * 5 + (cc + 2)] = (uint8_t)entry;
-            }
-            lds_barrier();                                                   // 4
-            RL_PHASE(2);
-            // 4. one wave composes the tables: correction after each near lane
-            if (wave == 0) {
-                uint32_t f = pack_ident();
-                if (lane < NN) {
-                    f = 0;
-                    for (int q = 0; q < 5; q++) f |= (uint32_t)sh.ntab[lane * 5 + q] << (3 * q);
-                }
-                f = wave_scan_u32(f, pack_ident(), [](uint32_t x, uint32_t y) { return compose(x, y); });
-                const uint32_t c0v = (f >> 6) & 7u;                          // entry for c = 0
-                const uint64_t smask = __ballot(lane < NN && c0v == STOPC);
-                if (lane < NN) sh.cafter[lane] = (int8_t)((int32_t)c0v - 2);
-                if (lane == 0) sh.stop_lane = smask ? sh.nlane[__ffsll((unsigned long long)smask) - 1] : (uint32_t)NC;
-            }
-            lds_barrier();                                                   // 5
-            RL_PHASE(3);
-            if (sh.stop_lane < eidx) eidx = sh.stop_lane;
-            // 5. every lane up to e: the exact step from its true predecessor
-            bool bad = false;
-            TbEval v{};
-            int64_t Dexp = 0;
-            if (mine && tid <= eidx) {
-                const int32_t cin = nrank > 0 ? (int32_t)sh.cafter[nrank - 1] : 0;
-                v = tb_eval(mode, D + Pj + cin, E, P, R, alive, add, cap, nd, profile);
-                const int32_t cout = near ? (nrank < MAX_NEAR ? (int32_t)sh.cafter[nrank] : 99) : cin;
-                Dexp = D + Pj + r + cout;
-                if (tid < eidx) bad = !(alive && v.inrange && !v.allowed && !v.clamped && v.Dact == Dexp);
-            }
-            const uint64_t bmask = __ballot(bad);
-            if (!loader && lane == 0)
-                sh.wbad[wave] = bmask ? (uint32_t)(wave * 64 + __ffsll((unsigned long long)bmask) - 1) : (uint32_t)NC;
-            lds_barrier();                                                   // 6
-            RL_PHASE(4);
-            {
-                const uint32_t mb = wave_min_u32(lane < (uint32_t)NWC ? sh.wbad[lane] : (uint32_t)NC);
-                eidx = mb < eidx ? mb : eidx;
-            }
-            // 6. commit lanes [first, e]; e's exact result is the next base
-            if (mine && tid <= eidx) write_out(a, i, tb_outputs(v, rq.n, rq.reset, cf.rate, cf.inv_rate));
-            if (tid == eidx) {
-                TbQ q = (v.inrange && mode == QM_DEC) || (v.inrange && mode == QM_BIN) ? TbQ{v.Dact, E}
-                                                                                     : tb_quant(v.tokens, profile);
-                sh.baseD = q.D;
-                sh.baseE = q.E;
-            }
-            lds_barrier();                                                   // 7
-            RL_PHASE(5);
-            first = eidx + 1;
-        }
-        if (loader) {          // chunk k+1 -> ring, start loading chunk k+2
-            st_fields((k + 1) & 1);
-            ld_fields(base + 2 * NC);
-        }
-        lds_barrier();
-    }
-    if (tid == 0) {
-        e->tok = tb_value(sh.baseD, sh.baseE, profile);
-        e->last = pre.lq[j1 - 1];
-        e->when = pre.when[j1 - 1];
-        if (dbg) { atomicAdd(&dbg[0], nrounds); atomicAdd(&dbg[1], nchunks); }
-#ifdef RL_STAMPS
-        if (dbg) {
-            atomicMax(&dbg[2], nrounds);
-            for (int q = 0; q < 6; q++) atomicMax((unsigned long long*)&dbg[8 + 2 * q], (unsigned long long)cyc[q]);
-        }
-#endif
-    }
-}
+#include "rl_tb_lanes.h"
+
+namespace rl {
 
 struct SegRec {
     uint32_t j0;
@@ -736,33 +407,60 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
             prev_when = expire_when(cfgs[in.cfg[ip]].ttl_tb, smsp);
         }
         const bool alive = key_alive(prev_when, sms, profile);
-        const double last = alive ? prev_last : now;
-        pre.add[j] = (now - last) * C.rate;
-        pre.alive[j] = alive ? 1 : 0;
+        pre.add[j] = alive ? (now - prev_last) * C.rate : __builtin_nan("");
+        const int64_t nv = in.n[i];
+        pre.nc[j] = ((uint64_t)c << 32) | (nv < (1LL << 31) ? (uint32_t)nv : 0u);
         pre.reset[j] = tb_reset_at(now, C);
         pre.lq[j] = lua_tostring_roundtrip(now, profile);
         pre.when[j] = expire_when(C.ttl_tb, sms);
     }
 }
 
-// results from sorted order back to the caller's order
-__global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-                                                   uint32_t m, uint32_t invalid_key, ReqArgs sorted, ReqArgs out) {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
-        if (sk[j] == invalid_key) continue;
-        uint32_t i = sv[j];
-        out.dec[i] = sorted.dec[j];
-        out.rem[i] = sorted.rem[j];
-        out.retry[i] = sorted.retry[j];
-        out.reset[i] = sorted.reset[j];
-        if (out.tok) out.tok[i] = sorted.tok[j];
+// Go's result arithmetic of a token-bucket step from the script's reply
+// (tokenbucket.go:114-130): Remaining = floor(tokens); RetryAfter from the
+// missing tokens when denied
+__device__ inline void tb_result(uint8_t dec, double tokens, int64_t n, const CfgDev& c, int64_t& rem,
+                                 int64_t& retry) {
+    rem = go_f2i(floor(tokens));
+    retry = 0;
+    if (dec == DEC_DENIED) {
+        const int64_t need = wsub(n, rem);
+        const double w = need == 1 ? c.inv_rate : (double)need / c.rate;   // tokensNeeded / refillRate
+        const int64_t d = go_f2i(w * 1e9);
+        retry = d < 0 ? 0 : d;
     }
 }
 
-// Work-queue replay: blocks first drain the heavy list (one segment per block,
-// cooperative), then the light list (256 segments per grab, one per thread).
-constexpr int COOP_NC = 448;                 // compute lanes per cooperative block
-constexpr int REPLAY_BLOCK = COOP_NC + 64;  // + one loader wave
+// results from sorted order back to the caller's order (token-bucket
+// remaining/retry_after are finished here, off the replay's critical path)
+__global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
+                                                   uint32_t m, uint32_t invalid_key, uint32_t win_base,
+                                                   const CfgDev* __restrict__ cfgs, ReqArgs sorted, ReqArgs out) {
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+        const uint32_t k0 = sk[j];
+        if (k0 == invalid_key) continue;
+        const uint32_t i = sv[j];
+        const uint8_t dec = sorted.dec[j];
+        const double tok = sorted.tok[j];
+        int64_t rem, retry;
+        if (k0 < win_base) {
+            tb_result(dec, tok, sorted.n[j], cfgs[sorted.cfg[j]], rem, retry);
+        } else {
+            rem = sorted.rem[j];
+            retry = sorted.retry[j];
+        }
+        out.dec[i] = dec;
+        out.rem[i] = rem;
+        out.retry[i] = retry;
+        out.reset[i] = sorted.reset[j];
+        if (out.tok) out.tok[i] = tok;
+    }
+}
+
+// Work-queue replay: blocks first drain the heavy list (one segment per block:
+// token bucket cooperatively, rl_tb_lanes.h), then the light list (one segment
+// per thread).
+constexpr int REPLAY_BLOCK = TB_NC + 64;    // 7 compute waves + 1 loader wave
 
 template <bool LCFG>
 __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
@@ -770,8 +468,8 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
     const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
     const CfgDev* __restrict__ gcfgs, uint32_t ncfg, int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
-    uint32_t* dbg) {
-    __shared__ CoopShared<COOP_NC> sh;
+    uint32_t* dbg, TbRuns runs) {
+    __shared__ LaneShared sh;
     __shared__ uint32_t s_u;
     __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
     if (LCFG) {
@@ -780,6 +478,9 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     }
     const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
     const uint32_t nheavy = *nheavy_p, nlight = *nlight_p;
+    // per-block phase timers (100 MHz realtime counter) -> debug maxima
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    uint32_t my_heavy = 0;
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
         __syncthreads();
@@ -788,13 +489,20 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
         if (u >= nheavy) break;
         const SegRec sg = heavy[u];
         const uint32_t k0 = sk[sg.j0];
+        const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
+        my_heavy++;
         if (k0 < win_base) {
-            replay_tb_coop<COOP_NC>(sh, &tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, dbg);
+            replay_tb_lanes(sh, &tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
         } else if (threadIdx.x == 0) {
             replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
         __syncthreads();
+#ifndef RL_STAMPS
+        if (threadIdx.x == 0 && dbg)
+            atomicMax(&dbg[8], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seg));
+#endif
     }
+    const uint64_t t_heavy = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)REPLAY_BLOCK);
         __syncthreads();
@@ -809,6 +517,13 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
             else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
     }
+#ifndef RL_STAMPS
+    if (threadIdx.x == 0 && dbg) {
+        atomicMax(&dbg[10], (uint32_t)(t_heavy - t_start));
+        atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_heavy));
+        atomicMax(&dbg[14], my_heavy);
+    }
+#endif
 }
 
 }  // namespace rl

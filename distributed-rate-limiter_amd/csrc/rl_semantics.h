@@ -31,6 +31,7 @@ enum : uint32_t {
     EF_ORDER = 2u,            // a live window key was evicted (per-key time went backwards)
     EF_LOOKBACK = 4u,         // radix-sort look-back spin bound hit
     EF_BAD_KEY = 8u,          // key id equal to the reserved empty marker
+    EF_INTERNAL = 16u,        // cooperative replay invariant violated (never expected)
 };
 
 // Per-config constants, precomputed on the host exactly as Go computes them.

@@ -54,10 +54,11 @@ class rl_stats(C.Structure):
         ("last_segments", C.c_uint64),
         ("last_heavy", C.c_uint64),
         ("last_coop_rounds", C.c_uint64),
-        ("last_coop_chunks", C.c_uint64),
+        ("last_coop_iters", C.c_uint64),
         ("sort_bits", C.c_uint32),
         ("sort_passes", C.c_uint32),
         ("stamp_cycles", C.c_uint64 * 7),
+        ("coop_ends", C.c_uint64 * 4),
     ]
 
 
