@@ -169,6 +169,7 @@ def main():
         raise SystemExit(f"engine error during timed region: {rc} {eng.last_error()}")
     stage_ms, nbat = eng.stage_times()
     st = eng.stats()
+    dbgw = eng.debug_words()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -208,7 +209,8 @@ def main():
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
-                          "coop_ends": [int(x) for x in st.coop_ends]},
+                          "coop_ends": [int(x) for x in st.coop_ends],
+                          "wave_phase_cycles": [int(x) * 16 for x in dbgw[24:72]]},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
                                                     (stage_ms / nbat).tolist())},
     }

@@ -136,9 +136,11 @@ namespace {
 constexpr int NSTAGES = 4;
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
-constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2,3] queue heads
-constexpr uint32_t CTRL_DBG = CTRL_NSEG + 4;   // [0] coop rounds [1] coop chunks [8..17] stamps
-constexpr uint32_t CTRL_WORDS = CTRL_DBG + 24;
+constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2] k_replay queue heads [3] k_tb_coop queue
+constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] iterations [2] max rounds [3..6] round ends
+                                               // [8..19] timers / stamps [24..71] per-wave stamps
+constexpr uint32_t CTRL_DBGN = 72;
+constexpr uint32_t CTRL_WORDS = CTRL_DBG + CTRL_DBGN;
 
 uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1;
@@ -187,6 +189,7 @@ struct rl_engine {
     int64_t* q_when = nullptr;
     SegRec* d_light = nullptr;
     int replay_grid = 2048;
+    int coop_grid = 512;        // k_tb_coop blocks (one per CU fits its LDS)
     uint32_t heavy_min = 32;   // segments this long replay cooperatively
     uint32_t* d_zero = nullptr;  // ctrl words + look-back status (memset per batch)
     size_t zero_bytes = 0;
@@ -266,8 +269,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
     size_t M = e->max_batch;
-    // q_add and q_nc carry 4 elements of slack: the replay's loader wave reads
-    // them in aligned 16-byte pairs that may end past the last request
+    // q_add and q_nc carry 128 elements of slack: the replay's loader wave
+    // reads them in aligned 128-element chunks that may end past the batch
     e->cfg_cap = 64;
     bool ok = true;
     ok &= hipMalloc(&e->d_cfg, sizeof(CfgDev) * e->cfg_cap) == hipSuccess;
@@ -287,8 +290,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->o_retry, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_tok, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_add, 8 * (M + 4)) == hipSuccess;
-    ok &= hipMalloc(&e->q_nc, 8 * (M + 4)) == hipSuccess;
+    ok &= hipMalloc(&e->q_add, 8 * (M + 128)) == hipSuccess;
+    ok &= hipMalloc(&e->q_nc, 8 * (M + 128)) == hipSuccess;
     ok &= hipMalloc(&e->runs.len, 2 * M) == hipSuccess;
     ok &= hipMalloc(&e->runs.E, 2 * M) == hipSuccess;
     ok &= hipMalloc(&e->runs.D0, 8 * M) == hipSuccess;
@@ -320,6 +323,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_REPLAY_GRID")) e->replay_grid = atoi(v);
+    if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
     *out = e;
@@ -419,16 +423,22 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
                                     pre);
     if (e->timing) (void)hipEventRecord(ev[3], s);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
-    if (ncfg <= (uint32_t)MAX_LCFG)
+    uint32_t* dbg = e->d_ctrl + CTRL_DBG;
+    if (ncfg <= (uint32_t)MAX_LCFG) {
+        k_tb_coop<true><<<e->coop_grid, TB_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, segctr + 4, e->win_base, e->d_tb,
+                                                          e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
+                                                          e->runs);
         k_replay<true><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                               segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
-                                                              ncfg, e->profile, ps, pre, e->d_eflags,
-                                                              e->d_ctrl + CTRL_DBG, e->runs);
-    else
+                                                              ncfg, e->profile, ps, pre, e->d_eflags, dbg);
+    } else {
+        k_tb_coop<false><<<e->coop_grid, TB_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, segctr + 4, e->win_base, e->d_tb,
+                                                           e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
+                                                           e->runs);
         k_replay<false><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                                segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
-                                                               ncfg, e->profile, ps, pre, e->d_eflags,
-                                                              e->d_ctrl + CTRL_DBG, e->runs);
+                                                               ncfg, e->profile, ps, pre, e->d_eflags, dbg);
+    }
     k_tb_expand<<<pgrid, 256, 0, s>>>(m, e->runs, e->d_cfg, e->profile, ps, pre, e->d_eflags);
     k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     if (e->timing) {
@@ -524,16 +534,17 @@ extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t 
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     if (!e || !out) return RL_EINVAL;
     (void)hipSetDevice(e->device);
-    uint32_t c[28] = {0};
+    uint32_t c[2] = {0, 0}, d[24] = {0};
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(c, e->d_ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 6; k++) e->stats.stamp_cycles[k] = ((uint64_t)c[4 + 8 + 2 * k + 1] << 32) | c[4 + 8 + 2 * k];
-    e->stats.stamp_cycles[6] = c[4 + 2];   // max rounds of one segment
+    HIPCHK(e, hipMemcpy(d, e->d_ctrl + CTRL_DBG, sizeof d, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 6; k++) e->stats.stamp_cycles[k] = ((uint64_t)d[8 + 2 * k + 1] << 32) | d[8 + 2 * k];
+    e->stats.stamp_cycles[6] = d[2];   // max rounds of one segment
     e->stats.last_heavy = c[0];
     e->stats.last_segments = (uint64_t)c[0] + c[1];
-    e->stats.last_coop_rounds = c[4];
-    e->stats.last_coop_iters = c[5];
-    for (int k = 0; k < 4; k++) e->stats.coop_ends[k] = c[4 + 3 + k];   // dbg[3..6]
+    e->stats.last_coop_rounds = d[0];
+    e->stats.last_coop_iters = d[1];
+    for (int k = 0; k < 4; k++) e->stats.coop_ends[k] = d[3 + k];
     *out = e->stats;
     return RL_OK;
 }
@@ -562,6 +573,16 @@ extern "C" int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint
     if (batches) *batches = e->timed_batches;
     for (int k = 0; k < NSTAGES; k++) e->stage_ms[k] = 0;
     e->timed_batches = 0;
+    return RL_OK;
+}
+
+// diagnostic: the last batch's replay debug words (include/rl_engine.h)
+extern "C" int rl_engine_debug_words(rl_engine* e, uint32_t* out, size_t n) {
+    if (!e || !out) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    if (n > CTRL_DBGN) n = CTRL_DBGN;
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpy(out, e->d_ctrl + CTRL_DBG, 4 * n, hipMemcpyDeviceToHost));
     return RL_OK;
 }
 

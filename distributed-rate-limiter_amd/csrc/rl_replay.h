@@ -316,16 +316,18 @@ __device__ inline int64_t readlane_i64(int64_t v, uint32_t l) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// one segment: the requests of one state-table slot, [j0, j0 + len) sorted
+struct SegRec {
+    uint32_t j0;
+    uint32_t len;
+};
+
 }  // namespace rl
 
 #include "rl_tb_lanes.h"
 
 namespace rl {
 
-struct SegRec {
-    uint32_t j0;
-    uint32_t len;
-};
 
 // segment heads -> (start, length), split into heavy (cooperative) and light
 // (one thread each) work lists.  One tile of SEG_TILE sorted positions per
@@ -457,10 +459,10 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
     }
 }
 
-// Work-queue replay: blocks first drain the heavy list (one segment per block:
-// token bucket cooperatively, rl_tb_lanes.h), then the light list (one segment
-// per thread).
-constexpr int REPLAY_BLOCK = TB_NC + 64;    // 7 compute waves + 1 loader wave
+// Work-queue replay of everything except heavy token-bucket segments (those
+// run in k_tb_coop): heavy window segments one per block (serial, thread 0),
+// then the light list, one segment per thread.
+constexpr int REPLAY_BLOCK = 256;
 
 template <bool LCFG>
 __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
@@ -468,8 +470,7 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
     const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
     const CfgDev* __restrict__ gcfgs, uint32_t ncfg, int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
-    uint32_t* dbg, TbRuns runs) {
-    __shared__ LaneShared sh;
+    uint32_t* dbg) {
     __shared__ uint32_t s_u;
     __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
     if (LCFG) {
@@ -478,9 +479,7 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
     }
     const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
     const uint32_t nheavy = *nheavy_p, nlight = *nlight_p;
-    // per-block phase timers (100 MHz realtime counter) -> debug maxima
-    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
-    uint32_t my_heavy = 0;
+    // heavy window segments: 64 per grab, one per block (serial replay by thread 0)
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
         __syncthreads();
@@ -489,20 +488,10 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
         if (u >= nheavy) break;
         const SegRec sg = heavy[u];
         const uint32_t k0 = sk[sg.j0];
-        const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
-        my_heavy++;
-        if (k0 < win_base) {
-            replay_tb_lanes(sh, &tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
-        } else if (threadIdx.x == 0) {
+        if (k0 >= win_base && threadIdx.x == 0)
             replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
-        }
-        __syncthreads();
-#ifndef RL_STAMPS
-        if (threadIdx.x == 0 && dbg)
-            atomicMax(&dbg[8], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seg));
-#endif
     }
-    const uint64_t t_heavy = __builtin_amdgcn_s_memrealtime();
+    const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)REPLAY_BLOCK);
         __syncthreads();
@@ -517,13 +506,7 @@ __global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
             else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
     }
-#ifndef RL_STAMPS
-    if (threadIdx.x == 0 && dbg) {
-        atomicMax(&dbg[10], (uint32_t)(t_heavy - t_start));
-        atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_heavy));
-        atomicMax(&dbg[14], my_heavy);
-    }
-#endif
+    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
 }
 
 }  // namespace rl

@@ -64,105 +64,113 @@ constexpr uint32_t NO_STOP = 0xffffffffu;
 // in order; this keeps the compiler from reordering around it)
 __device__ inline void wave_lds_fence() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// cooperative replay geometry: NC compute lanes (7 waves) + 1 loader wave
-constexpr int TB_NC = 448;
-constexpr int TB_K = 8;                          // requests per lane per round
+// cooperative replay geometry: NC compute lanes + 1 loader wave
+#ifndef RL_TB_NC
+#define RL_TB_NC 448
+#endif
+#ifndef RL_TB_K
+#define RL_TB_K 8
+#endif
+constexpr int TB_NC = RL_TB_NC;
+constexpr int TB_K = RL_TB_K;                    // requests per lane per round
 constexpr int TB_NW = TB_NC / 64;
 constexpr uint32_t TB_WIN = (uint32_t)TB_NC * TB_K;
-// LDS ring of request inputs, by absolute sorted position; padded so that
-// lanes reading positions l*K+q (fixed q) hit distinct banks
-constexpr uint32_t RING = 8192;
-constexpr uint32_t RING_SLOTS = RING + RING / TB_K;
-__host__ __device__ constexpr uint32_t ring_idx(uint32_t p) {
-    return (p & (RING - 1)) + ((p & (RING - 1)) / TB_K);
-}
-static_assert(RING >= 2 * TB_WIN, "the ring must hold the next window while the current one is read");
+// LDS ring of request inputs by absolute sorted position, in 16-byte
+// granules (two positions).  Granule G lives in slot swz(G mod RING_G): an XOR
+// of its column (G mod 16) with bits 4-5, so the 8 lanes of one ds_read_b128
+// cycle (lane l reads granule G0 + 4l + j) always hit distinct banks, while a
+// row of 16 slots still holds 16 consecutive granules (the loader's LDS-DMA
+// writes slots lane-linearly and swizzles the SOURCE address instead).
+constexpr uint32_t RING = 8192;                  // positions
+constexpr uint32_t RING_G = RING / 2;            // granules
+__host__ __device__ constexpr uint32_t swz(uint32_t g) { return (g & ~15u) | ((g & 15u) ^ ((g >> 4) & 3u)); }
+__host__ __device__ constexpr uint32_t ring_slot(uint32_t granule) { return swz(granule & (RING_G - 1)); }
+static_assert(RING >= 2 * TB_WIN + 256, "the ring must hold the next window while the current one is read");
+
+constexpr uint32_t NL_MAX = 512;   // near steps resolved per round
 
 struct LaneShared {
-    double r_add[RING_SLOTS];
-    uint64_t r_nc[RING_SLOTS];   // TbPre::nc
+    double2 r_add[RING_G];       // TbPre::add
+    ulonglong2 r_nc[RING_G];     // TbPre::nc
     int64_t wtot[TB_NW];         // lane-sum scan
-    int64_t itot[TB_NW];         // offset-delta scan (per iteration)
-    uint32_t ich[TB_NW];         // first lane whose delta changed
-    uint32_t ibk[TB_NW];         // first lane that breaks
+    uint32_t ntot[TB_NW];        // near-step count scan
     uint32_t wmin[TB_NW];        // first stop
+    // the round's near steps in sequence order (NL_MAX at most)
+    double nl_pred[NL_MAX];      // nominal predecessor state
+    double nl_add[NL_MAX];
+    uint64_t nl_nc[NL_MAX];      // TbPre::nc
+    int32_t nl_off[NL_MAX];      // resolved: offset after the step (true - nominal)
+    uint32_t nstop;              // first near step that stops the round (list index)
     int64_t baseD[2];            // round-parity double buffer
     int32_t baseE[2];
     uint32_t first[2];
 };
 
-// The loader wave: streams TbPre::{add, nc} of the segment into the ring,
-// up to RING positions ahead of the current window.  Each pump() retires the
-// chunk issued by the previous pump (its latency elapsed behind a compute
-// phase) into LDS and issues the next one; pump() runs in every gap between
-// two block barriers, so the loader keeps pace with no wait of its own.  It
-// writes only positions >= the window's end, i.e. ring slots of positions
-// already consumed.
-constexpr int LD_CH = 4;                 // 128-position chunks per pump
+__device__ inline double ring_add(const LaneShared& sh, uint32_t p) {
+    const double2 g = sh.r_add[ring_slot(p >> 1)];
+    return (p & 1u) ? g.y : g.x;
+}
+__device__ inline uint64_t ring_nc(const LaneShared& sh, uint32_t p) {
+    const ulonglong2 g = sh.r_nc[ring_slot(p >> 1)];
+    return (p & 1u) ? g.y : g.x;
+}
+
+// The loader wave streams TbPre::{add, nc} into the ring in 128-position
+// chunks by LDS-DMA (global_load_lds_dwordx4: no registers, lands
+// asynchronously).  It issues every chunk the ring can take right after a
+// round starts and waits for them only at the round's end, so the loads land
+// behind a whole round of compute.  A chunk may only overwrite positions
+// already consumed: chunk c is allowed once 128c + 128 <= first + RING.
+// The source arrays carry 128 elements of slack past the batch.
 struct TbLoader {
-    uint32_t fill;                       // positions < fill are in the ring (even unless == j1)
-    uint32_t pg, pend_end;               // issued, not yet written: [pg, pend_end)
-    bool pend;
-    double2 pa[LD_CH];
-    ulonglong2 pn[LD_CH];
+    uint32_t next;       // next chunk to issue
+    uint32_t issued;     // chunks issued since the last wait
 };
 
-__device__ __attribute__((always_inline)) inline void ld_retire(TbLoader& L, LaneShared& sh, uint32_t lane) {
-    if (!L.pend) return;
-#pragma unroll
-    for (int c = 0; c < LD_CH; c++) {
-        const uint32_t g = L.pg + c * 128 + 2 * lane;
-        if (g < L.pend_end) {
-            sh.r_add[ring_idx(g)] = L.pa[c].x;
-            sh.r_nc[ring_idx(g)] = L.pn[c].x;
-        }
-        if (g + 1 < L.pend_end) {
-            sh.r_add[ring_idx(g + 1)] = L.pa[c].y;
-            sh.r_nc[ring_idx(g + 1)] = L.pn[c].y;
-        }
+// one 16-byte LDS-DMA per lane into the slots starting at the wave-uniform
+// LDS byte address `lds` (issued from asm: hipcc neither counts it nor drains
+// it early; ld_until waits for it explicitly)
+__device__ __attribute__((always_inline)) inline void glds16(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    __asm__ volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(gsrc), "s"(lds)
+                     : "memory");
+}
+
+__device__ __attribute__((always_inline)) inline void ld_chunk(LaneShared& sh, uint32_t c, const TbPre& pre,
+                                                              uint32_t lane) {
+    const uint32_t s0 = (c * 64u) & (RING_G - 1);   // first slot of the chunk (row aligned)
+    const uint32_t g = c * 64u + swz(lane);         // granule this lane's slot holds
+    const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&sh.r_add[s0];
+    const uint32_t ln = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&sh.r_nc[s0];
+    glds16(pre.add + 2u * g, __builtin_amdgcn_readfirstlane(la));
+    glds16(pre.nc + 2u * g, __builtin_amdgcn_readfirstlane(ln));
+}
+
+// issue every chunk the ring can take for a window starting at `first`
+__device__ __attribute__((always_inline)) inline void ld_issue(TbLoader& L, LaneShared& sh, uint32_t first,
+                                                              uint32_t j1, const TbPre& pre, uint32_t lane) {
+    const uint32_t lim = (first + RING) / 128u;     // chunks c < lim fit
+    const uint32_t endc = (j1 + 127u) / 128u;
+    while (L.next < lim && L.next < endc && L.issued < 28u) {   // <= 56 outstanding (vmcnt <= 63)
+        ld_chunk(sh, L.next, pre, lane);
+        L.next++;
+        L.issued++;
     }
-    L.fill = L.pend_end;
-    L.pend = false;
 }
 
-__device__ __attribute__((always_inline)) inline void ld_issue(TbLoader& L, uint32_t limit, const TbPre& pre, uint32_t lane) {
-    if (L.pend || L.fill >= limit) return;
-    L.pg = L.fill;
-    L.pend_end = (limit - L.fill) < (uint32_t)(LD_CH * 128) ? limit : L.fill + LD_CH * 128;
-#pragma unroll
-    for (int c = 0; c < LD_CH; c++) {
-        const uint32_t g = L.pg + c * 128 + 2 * lane;     // even: 16-byte aligned pair
-        if (g < L.pend_end) {
-            L.pa[c] = *reinterpret_cast<const double2*>(pre.add + g);
-            L.pn[c] = *reinterpret_cast<const ulonglong2*>(pre.nc + g);
-        }
+// make [.., target) resident: issue what is missing and wait for everything
+__device__ __attribute__((always_inline)) inline void ld_until(TbLoader& L, LaneShared& sh, uint32_t first,
+                                                              uint32_t target, uint32_t j1, const TbPre& pre,
+                                                              uint32_t lane) {
+    const uint32_t need = ((target < j1 ? target : j1) + 127u) / 128u;
+    for (;;) {
+        ld_issue(L, sh, first, j1, pre, lane);
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        L.issued = 0;
+        if (L.next >= need) break;
     }
-    L.pend = true;
-}
-
-// fill limit for a window starting at `first`: RING ahead, even-aligned
-__device__ __attribute__((always_inline)) inline uint32_t ld_limit(uint32_t first, uint32_t j1) {
-    const uint32_t lim = (first + RING) & ~1u;
-    return lim < j1 ? lim : j1;
-}
-
-__device__ __attribute__((always_inline)) inline void ld_pump(TbLoader& L, LaneShared& sh, uint32_t first, uint32_t j1, const TbPre& pre,
-                               uint32_t lane) {
-    ld_retire(L, sh, lane);
-    ld_issue(L, ld_limit(first, j1), pre, lane);
-}
-
-// synchronous: make sure [.., target) is in the ring (the next window)
-__device__ __attribute__((always_inline)) inline void ld_until(TbLoader& L, LaneShared& sh, uint32_t first, uint32_t target, uint32_t j1,
-                                const TbPre& pre, uint32_t lane) {
-    const uint32_t lim = ld_limit(first, j1);
-    if (target > lim) target = lim;
-    while (L.fill < target) {
-        ld_retire(L, sh, lane);
-        ld_issue(L, lim, pre, lane);
-    }
-    ld_retire(L, sh, lane);
-    ld_issue(L, lim, pre, lane);
 }
 
 // RNE(x * P) as an exact integer-valued double (x*P < 2^52), P = 10^k exact
@@ -215,6 +223,64 @@ struct TbRuns {
     int64_t* D1;         // exact stored state after it, as the chain resolved it
 };
 
+// Resolution of a round's near steps (list order = sequence order), by ONE
+// wave, 64 steps at a time.  A step's exact result depends on its exact
+// predecessor = nominal + (offset before it); far steps keep the offset, so
+// the offset before step k is the batch's entry offset plus the flips
+// (exact result - nominal result) of the batch's earlier steps.  Wave-local
+// fixed point: evaluate every step at the current guess, scan the flips
+// (DPP), re-guess; when no guess changes (before the first step that leaves
+// the regime) the guesses are the true offsets, by induction over lanes.
+// Writes nl_off[k] for every resolved step and nstop = the first step that
+// stops the round (leaves the regime, or the iteration cap), else NO_STOP.
+template <int MODE>
+__device__ __attribute__((noinline)) void tb_near_resolve(LaneShared& sh, uint32_t nl, double P, double R,
+                                                          const CfgDev* __restrict__ cfgs, uint32_t& iters) {
+    constexpr int ITMAX = 16;
+    const uint32_t lane = threadIdx.x & 63;
+    int32_t cb = 0;                   // offset before the batch (exact)
+    uint32_t nstop = NO_STOP;
+    for (uint32_t b = 0; b < nl; b += 64) {
+        const uint32_t k = b + lane;
+        const bool v = k < nl;
+        const double pn = v ? sh.nl_pred[k] : 0.0;
+        const double ad = v ? sh.nl_add[k] : 0.0;
+        const uint64_t w = v ? sh.nl_nc[k] : 1ull;
+        const double cap = cfgs[(uint32_t)(w >> 32)].limit_d, nd = (double)(uint32_t)w;
+        const double r = rint(ad * P);
+        int32_t est = 0, flip = 0;
+        uint32_t stop_lane = 64;
+        for (int it = 0;; it++) {
+            double tk;
+            const double pred = pn + (double)(cb + est);
+            const double Dn = tb_step_d<MODE>(pred, P, R, ad, cap, nd, tk);
+            const bool brk = v && !(Dn == Dn);
+            flip = (!v || brk) ? 0 : (int32_t)(Dn - (pred + r));
+            const int32_t incl = (int32_t)wave_scan_u32((uint32_t)flip, 0u,
+                                                        [](uint32_t x, uint32_t y) { return x + y; });
+            const int32_t en = incl - flip;
+            const uint64_t bm = __ballot(brk);
+            const uint64_t cm = __ballot(v && en != est);
+            const uint32_t fb = bm ? (uint32_t)__ffsll((unsigned long long)bm) - 1 : 64u;
+            const uint32_t fc = cm ? (uint32_t)__ffsll((unsigned long long)cm) - 1 : 64u;
+            iters++;
+            if (fc >= fb) { stop_lane = fb; break; }             // converged up to the first break
+            if (it + 1 == ITMAX) {                               // lanes < fc are exact
+                stop_lane = fc;
+                break;
+            }
+            est = en;
+        }
+        if (v && lane < stop_lane) sh.nl_off[k] = cb + est + flip;
+        if (stop_lane < 64) {
+            nstop = b + stop_lane;
+            break;
+        }
+        cb += __builtin_amdgcn_readlane(est + flip, 63);
+    }
+    if (lane == 0) sh.nstop = nstop;
+}
+
 // One round in a fast mode.  Reads the base state from parity slot `par`,
 // publishes the next base into slot par^1; the caller's barrier ends the
 // round.  Positions past the segment end are phantoms (add 0, live, never
@@ -226,7 +292,6 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     uint64_t* cyc, uint32_t& iters, TbLoader& L, uint32_t* dbg, const TbRuns& runs) {
     constexpr int NW = TB_NW, K = TB_K;
     constexpr uint32_t WIN = TB_WIN;
-    constexpr int ITMAX = 8;
     const double LO = MODE == QM_DEC ? (double)DEC_LO : (double)BIN_LO;
     const double HI = MODE == QM_DEC ? (double)DEC_HI : (double)BIN_HI;
     uint64_t t0 = 0, t1 = 0;
@@ -251,19 +316,38 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     int64_t nn[K];
     uint32_t cfq[K];
     uint32_t deadm = 0, nearm = 0, hardm = 0;
+    {
+        // my positions [i0, i0 + K): K/2 granules, one more when i0 is odd
+        // (first is block-uniform, so is the parity)
+        double ga[K + 2];
+        uint64_t gn[K + 2];
+        const uint32_t g0 = i0 >> 1;
 #pragma unroll
-    for (int q = 0; q < K; q++) {
-        const bool v = (uint32_t)q < nvalid;
-        const uint32_t si = ring_idx(i0 + q);
-        const double x = sh.r_add[si];
-        const uint64_t w = sh.r_nc[si];
-        if (v && !(x == x)) deadm |= 1u << q;           // NaN: key expired / absent
-        if (v && (uint32_t)w == 0u) hardm |= 1u << q;   // n >= 2^31: exact path
-        add[q] = v && x == x ? x : 0.0;
-        nn[q] = v ? (int64_t)(uint32_t)w : 1;
-        cfq[q] = v ? (uint32_t)(w >> 32) : 0u;
+        for (int j = 0; j < K / 2 + 1; j++) {
+            if (j < K / 2 || (i0 & 1u)) {
+                const double2 x = sh.r_add[ring_slot(g0 + j)];
+                const ulonglong2 y = sh.r_nc[ring_slot(g0 + j)];
+                ga[2 * j] = x.x; ga[2 * j + 1] = x.y;
+                gn[2 * j] = y.x; gn[2 * j + 1] = y.y;
+            } else {
+                ga[2 * j] = ga[2 * j + 1] = 0.0;
+                gn[2 * j] = gn[2 * j + 1] = 0;
+            }
+        }
+        const uint32_t o = i0 & 1u;
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            const bool v = (uint32_t)q < nvalid;
+            const double x = o ? ga[q + 1] : ga[q];
+            const uint64_t w = o ? gn[q + 1] : gn[q];
+            if (v && !(x == x)) deadm |= 1u << q;           // NaN: key expired / absent
+            if (v && (uint32_t)w == 0u) hardm |= 1u << q;   // n >= 2^31: exact path
+            add[q] = v && x == x ? x : 0.0;
+            nn[q] = v ? (int64_t)(uint32_t)w : 1;
+            cfq[q] = v ? (uint32_t)(w >> 32) : 0u;
+        }
     }
-    if (loader) ld_pump(L, sh, first, j1, pre, lane);
+    if (loader) ld_issue(L, sh, first, j1, pre, lane);
     double S = 0.0;
     float dq[K];         // distance of add/u from the nearest integer (near candidates)
 #pragma unroll
@@ -295,7 +379,6 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     if (lane == 63 && !loader) sh.wtot[wave] = inc;
     lds_barrier();                                                        // B1
     RL_PHASE(1);
-    if (loader) ld_pump(L, sh, first, j1, pre, lane);
     int64_t pre_w = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++)
@@ -318,115 +401,77 @@ __device__ __attribute__((always_inline)) inline void tb_round(
         nearm = nm;
     }
 
-    // C. true start offsets by fixed-point iteration.  My end offset as a
-    // function of my start offset s: far steps keep it, near steps are
-    // evaluated exactly (dl[q]: the offset change at near step q); `brk` = a
-    // near step leaves the regime or a stop request ends the lane.
-    double dl[K];
-    uint32_t bq = K;     // the near step that left the regime (K: none)
-    auto near_walk = [&](double s, bool& brk) -> double {
-        double c = s;
-        bq = K;
+    // C. near steps: compacted into an LDS list in sequence order, resolved
+    // by wave 0 (tb_near_resolve), read back as offsets
+    const uint32_t ncnt = (uint32_t)__popc(nearm);
+    const uint32_t ninc = wave_scan_u32(ncnt, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    if (lane == 63 && !loader) sh.ntot[wave] = ninc;
+    lds_barrier();                                                        // B2
+    uint32_t rank0 = ninc - ncnt, nl = 0;
 #pragma unroll
-        for (int k = 0; k < K; k++) dl[k] = 0.0;
-        uint32_t todo = nearm;
-        while (todo) {
-            const uint32_t q = (uint32_t)__builtin_ctz(todo);
-            todo &= todo - 1u;
-            double xa = 0.0, xc = 0.0, xp = 0.0, nd = 1.0;
-            uint32_t xcf = 0;
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                if ((uint32_t)k == q) {
-                    xa = add[k];
-                    nd = (double)nn[k];
-                    xcf = cfq[k];
-                    xc = cum[k];
-                    xp = k ? cum[k - 1] : 0.0;
-                }
-            double tk;
-            const double Dn = tb_step_d<MODE>(Nb + xp + c, P, R, xa, cfgs[xcf].limit_d, nd, tk);
-            if (!(Dn == Dn)) { bq = q; break; }
-            const double cn = Dn - (Nb + xc);
-#pragma unroll
-            for (int k = 0; k < K; k++)
-                if ((uint32_t)k == q) dl[k] = cn - c;
-            c = cn;
-        }
-        brk = evq < (uint32_t)K || bq < (uint32_t)K;
-        return c;
-    };
-    // Iteration k: starts s^k = scan of the deltas taken at s^(k-1).  When no
-    // delta (before the first break) changes at s^k, the starts are a fixed
-    // point and, by induction over lanes, TRUE.  At the cap, lanes up to the
-    // first changed one still have true starts; the round ends after it.
-    bool brk;
-    double soff = 0.0;
-    double cend = near_walk(0.0, brk);
-    RL_PHASE(2);
-    uint32_t unstable = NO_STOP;
-    for (int it = 0;; it++) {
-        const double dd = cend - soff;
-        const int64_t di = (brk || !(fabs(dd) < 4e18)) ? 0 : (int64_t)dd;
-        const int64_t dinc = wave_incl_scan_i64(di);
-        if (lane == 63 && !loader) sh.itot[wave] = dinc;
-        lds_barrier();
-        int64_t dw = 0;
-#pragma unroll
-        for (int w = 0; w < NW; w++)
-            if (w < (int)wave) dw += sh.itot[w];
-        const double snew = (double)(dw + dinc - di);
-        bool changed = false;
-        if (snew != soff) {
-            const double dold = cend - soff;
-            const bool bold = brk;
-            cend = nearm ? near_walk(snew, brk) : cend + (snew - soff);
-            changed = brk != bold || (!brk && cend - snew != dold);
-            soff = snew;
-        }
-        const uint32_t fch = wave_min_u32(changed && nvalid ? tid : NO_STOP);
-        const uint32_t fbk = wave_min_u32(brk && nvalid ? tid : NO_STOP);
-        if (lane == 0 && !loader) { sh.ich[wave] = fch; sh.ibk[wave] = fbk; }
-        lds_barrier();
-        if (loader) ld_pump(L, sh, first, j1, pre, lane);
-        uint32_t ch = NO_STOP, bk = NO_STOP;
-#pragma unroll
-        for (int w = 0; w < NW; w++) {
-            ch = sh.ich[w] < ch ? sh.ich[w] : ch;
-            bk = sh.ibk[w] < bk ? sh.ibk[w] : bk;
-        }
-        iters++;
-        if (ch == NO_STOP || ch >= bk) break;                 // block-uniform
-        if (it + 1 == ITMAX) { unstable = ch; break; }
+    for (int w = 0; w < NW; w++) {
+        if (w < (int)wave) rank0 += sh.ntot[w];
+        nl += sh.ntot[w];
     }
+    {
+        uint32_t k = rank0;
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            if ((nearm >> q) & 1u) {
+                if (k < NL_MAX) {
+                    sh.nl_pred[k] = Nb + (q ? cum[q - 1] : 0.0);
+                    sh.nl_add[k] = add[q];
+                    sh.nl_nc[k] = ((uint64_t)cfq[q] << 32) | (uint32_t)nn[q];
+                }
+                k++;
+            }
+        }
+    }
+    lds_barrier();                                                        // B3
+    RL_PHASE(2);
+    if (wave == 0) tb_near_resolve<MODE>(sh, nl < NL_MAX ? nl : NL_MAX, P, R, cfgs, iters);
+    lds_barrier();                                                        // B4
     RL_PHASE(3);
+    // list capacity: the step of rank NL_MAX stops too (its predecessor is known)
+    const uint32_t nstop = nl > NL_MAX && sh.nstop > NL_MAX ? NL_MAX : sh.nstop;
 
     // D. every request's next state from my true start; the first one that
     // may leave the regime stops the lane (near steps were checked exactly)
-    uint32_t stopq = evq < bq ? evq : bq;
-    double spred = 0.0, Dlast = Nb + soff;
+    uint32_t stopq = evq;
+    double spred = 0.0;
+    // my start offset: the offset after the last near step before my lane
+    const double cstart = (rank0 > 0 && rank0 - 1 < nstop) ? (double)sh.nl_off[rank0 - 1] : 0.0;
+    double Dlast = Nb + cstart;
     {
-        double c = soff;
+        double c = cstart;
+        uint32_t k = rank0;
 #pragma unroll
         for (int q = 0; q < K; q++) {
             const double pred = Nb + (q ? cum[q - 1] : 0.0) + c;
             if ((uint32_t)q == stopq) spred = pred;
             if ((uint32_t)q < stopq) {
-                c += dl[q];
-                const double Dn = Nb + cum[q] + c;
-                // decade: exact; allow / clamp: |tokens - D'u| <= 0.53 u
-                const double vhi = (Dn + 2.0) * R * (1.0 + 1e-9);
-                bool ev = !(fabs(Dn) >= LO && fabs(Dn) < HI);
-                ev = ev || !(vhi < (double)nn[q]) || !(vhi < cfgs[cfq[q]].limit_d);
-                if (ev && !((nearm >> q) & 1u) && (uint32_t)q < nvalid) {
+                bool ev;
+                if ((nearm >> q) & 1u) {
+                    ev = k >= nstop;
+                    if (!ev) c = (double)sh.nl_off[k];
+                    k++;
+                } else {
+                    const double Dn = Nb + cum[q] + c;
+                    // decade: exact; allow / clamp: |tokens - D'u| <= 0.53 u
+                    const double vhi = (Dn + 2.0) * R * (1.0 + 1e-9);
+                    ev = !(fabs(Dn) >= LO && fabs(Dn) < HI);
+                    ev = ev || !(vhi < (double)nn[q]) || !(vhi < cfgs[cfq[q]].limit_d);
+                }
+                if (ev && (uint32_t)q < nvalid) {
                     stopq = q;
                     spred = pred;
                 } else {
-                    Dlast = Dn;
+                    Dlast = Nb + cum[q] + c;
                 }
             }
         }
     }
+    const uint32_t unstable = NO_STOP;
     // stop key: (position << 1) | kind; kind 0 = boundary after committed
     // requests (wins ties), 1 = a stop request stepped exactly by its owner
     uint32_t sg = NO_STOP;
@@ -460,7 +505,7 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     if (len) {
         runs.len[i0] = (uint16_t)len;
         runs.E[i0] = (int16_t)E;
-        runs.D0[i0] = (int64_t)(Nb + soff);
+        runs.D0[i0] = (int64_t)(Nb + cstart);
         runs.D1[i0] = (int64_t)Dlast;
     }
     if (estep) {
@@ -502,8 +547,8 @@ __device__ __attribute__((always_inline)) inline void replay_tb_lanes(
     uint32_t nrounds = 0, niters = 0, par = 0;
     uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};
     TbLoader L;
-    L.fill = j0 & ~1u;
-    L.pend = false;
+    L.next = j0 / 128u;
+    L.issued = 0;
     if (tid == 0) {
         const TbQ q = tb_quant(e->tok, profile);
         sh.baseD[0] = q.D;
@@ -531,10 +576,10 @@ __device__ __attribute__((always_inline)) inline void replay_tb_lanes(
             // off the fast decades (or an empty/zero state): one exact step
             if (tid == 0) {
                 const uint32_t i = first;
-                const uint64_t w = sh.r_nc[ring_idx(i)];
+                const uint64_t w = ring_nc(sh, i);
                 const CfgDev& C = cfgs[(uint32_t)(w >> 32)];
                 const int64_t nn = (uint32_t)w ? (int64_t)(uint32_t)w : a.n[i];
-                const double add = sh.r_add[ring_idx(i)];
+                const double add = ring_add(sh, i);
                 const bool alive = add == add;
                 const TbEval v = tb_eval(QM_NONE, D, E, 1.0, 1.0, alive, alive ? add : 0.0, C.limit_d,
                                          (double)nn, profile);
@@ -550,9 +595,9 @@ __device__ __attribute__((always_inline)) inline void replay_tb_lanes(
         lds_barrier();                                                        // B4
     }
 #ifdef RL_STAMPS
-    // every wave reports: the max over waves of each phase shows who waits
+    // every wave reports its own phase sums (16-cycle units), longest segment
     if ((tid & 63) == 0 && dbg)
-        for (int k = 0; k < 6; k++) atomicMax(&dbg[8 + 2 * k], (uint32_t)(cyc[k] >> 4));   // 16-cycle units
+        for (int k = 0; k < 6; k++) atomicMax(&dbg[24 + 6 * (tid >> 6) + k], (uint32_t)(cyc[k] >> 4));
 #endif
     if (tid == 0) {
         e->tok = tb_value(sh.baseD[par], sh.baseE[par], profile);
@@ -604,6 +649,47 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, cons
             }
         }
         if (!ok || D != (double)runs.D1[j]) atomicOr(eflags, EF_INTERNAL);
+    }
+}
+
+// Cooperative replay of the heavy token-bucket segments: one segment per
+// block from a work queue (window segments in the heavy list are k_replay's).
+constexpr int TB_BLOCK = TB_NC + 64;    // 7 compute waves + 1 loader wave
+
+template <bool LCFG>
+__global__ __launch_bounds__(TB_BLOCK) void k_tb_coop(const uint32_t* __restrict__ sk,
+                                                      const SegRec* __restrict__ heavy,
+                                                      const uint32_t* __restrict__ nheavy_p, uint32_t* qctr,
+                                                      uint32_t win_base, TbEntry* tb,
+                                                      const CfgDev* __restrict__ gcfgs, uint32_t ncfg,
+                                                      int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
+                                                      uint32_t* dbg, TbRuns runs) {
+    __shared__ LaneShared sh;
+    __shared__ uint32_t s_u;
+    __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
+    if (LCFG) {
+        for (uint32_t c = threadIdx.x; c < ncfg; c += blockDim.x) s_cfg[c] = gcfgs[c];
+        __syncthreads();
+    }
+    const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
+    const uint32_t nheavy = *nheavy_p;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            uint32_t u;
+            do {   // skip window segments (k_replay's)
+                u = atomicAdd(qctr, 1u);
+            } while (u < nheavy && sk[heavy[u].j0] >= win_base);
+            s_u = u;
+        }
+        __syncthreads();
+        const uint32_t u = s_u;
+        __syncthreads();
+        if (u >= nheavy) break;
+        const SegRec sg = heavy[u];
+        const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
+        replay_tb_lanes(sh, &tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
+        __syncthreads();
+        if (threadIdx.x == 0 && dbg) atomicMax(&dbg[8], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seg));
     }
 }
 

@@ -85,6 +85,7 @@ _sig = {
     "rl_engine_set_timing": (C.c_int, [vp, C.c_int]),
     "rl_engine_stage_times": (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_uint64)]),
     "rl_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
+    "rl_engine_debug_words": (C.c_int, [vp, vp, C.c_size_t]),
     "rl_selftest_q14_host": (C.c_int, [vp, vp, C.c_size_t]),
     "rl_selftest_q14_device": (C.c_int, [vp, vp, vp, C.c_size_t]),
     "rll_engine_new": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp), C.c_char_p, C.c_size_t]),
@@ -207,6 +208,11 @@ class Engine:
         s = rl_stats()
         lib.rl_engine_stats(self.h, C.byref(s))
         return s
+
+    def debug_words(self, n=72) -> np.ndarray:
+        out = np.zeros(n, np.uint32)
+        lib.rl_engine_debug_words(self.h, _ptr(out), n)
+        return out
 
     def set_timing(self, on: bool):
         lib.rl_engine_set_timing(self.h, 1 if on else 0)

@@ -10,4 +10,9 @@ print(sys.argv[1], "| %.1f M/s" % (d["value"] / 1e6),
       {k: round(x, 3) for k, x in d["stages_ms_per_batch"].items()},
       "timers_us", [round(x / 100, 1) for x in r["stamp_cycles_longest_segment"][:6]], "rounds", r["coop_rounds"], "iters", r["coop_iters"],
       "maxr", r["stamp_cycles_longest_segment"][6], "ends", r.get("coop_ends"))
+w = r.get("wave_phase_cycles", [])
+if any(w):
+    n = max(1, r["stamp_cycles_longest_segment"][6])
+    for k in range(8):
+        print("  wave", k, "cycles/round per phase", [round(x / n) for x in w[6 * k:6 * k + 6]])
 PY
