@@ -210,7 +210,7 @@ def main():
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
                           "coop_ends": [int(x) for x in st.coop_ends],
-                          "wave_phase_cycles": [int(x) * 16 for x in dbgw[24:72]]},
+                          "wave_phase_cycles": [int(x) * 16 for x in dbgw[24:88]]},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
                                                     (stage_ms / nbat).tolist())},
     }

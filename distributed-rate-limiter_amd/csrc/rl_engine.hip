@@ -138,8 +138,8 @@ constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
 constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2] k_replay queue heads [3] k_tb_coop queue
 constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] iterations [2] max rounds [3..6] round ends
-                                               // [8..19] timers / stamps [24..71] per-wave stamps
-constexpr uint32_t CTRL_DBGN = 72;
+                                               // [8..19] timers / stamps [24..87] per-wave stamps
+constexpr uint32_t CTRL_DBGN = 88;
 constexpr uint32_t CTRL_WORDS = CTRL_DBG + CTRL_DBGN;
 
 uint64_t pow2_at_least(uint64_t v) {

@@ -347,6 +347,7 @@ __device__ __attribute__((always_inline)) inline void tb_round(
             cfq[q] = v ? (uint32_t)(w >> 32) : 0u;
         }
     }
+    RL_PHASE(0);
     if (loader) ld_issue(L, sh, first, j1, pre, lane);
     double S = 0.0;
     float dq[K];         // distance of add/u from the nearest integer (near candidates)
@@ -371,14 +372,14 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     const uint32_t evm = deadm | hardm;
     const uint32_t evq = evm ? (uint32_t)__builtin_ctz(evm) : (uint32_t)K;
     nearm &= evq >= 32 ? ~0u : ((1u << evq) - 1u);
-    RL_PHASE(0);
+    RL_PHASE(1);
 
     // B. block exclusive scan of the lane sums (int64: exact at any size)
     const int64_t Si = (int64_t)S;
     const int64_t inc = wave_incl_scan_i64(Si);
     if (lane == 63 && !loader) sh.wtot[wave] = inc;
     lds_barrier();                                                        // B1
-    RL_PHASE(1);
+    RL_PHASE(2);
     int64_t pre_w = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++)
@@ -407,6 +408,7 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     const uint32_t ninc = wave_scan_u32(ncnt, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     if (lane == 63 && !loader) sh.ntot[wave] = ninc;
     lds_barrier();                                                        // B2
+    RL_PHASE(3);
     uint32_t rank0 = ninc - ncnt, nl = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -428,10 +430,10 @@ __device__ __attribute__((always_inline)) inline void tb_round(
         }
     }
     lds_barrier();                                                        // B3
-    RL_PHASE(2);
+    RL_PHASE(4);
     if (wave == 0) tb_near_resolve<MODE>(sh, nl < NL_MAX ? nl : NL_MAX, P, R, cfgs, iters);
     lds_barrier();                                                        // B4
-    RL_PHASE(3);
+    RL_PHASE(5);
     // list capacity: the step of rank NL_MAX stops too (its predecessor is known)
     const uint32_t nstop = nl > NL_MAX && sh.nstop > NL_MAX ? NL_MAX : sh.nstop;
 
@@ -481,8 +483,8 @@ __device__ __attribute__((always_inline)) inline void tb_round(
     }
     const uint32_t wm = wave_min_u32(sg);
     if (lane == 0 && !loader) sh.wmin[wave] = wm;
-    lds_barrier();                                                        // B3
-    RL_PHASE(4);
+    lds_barrier();                                                        // B5
+    RL_PHASE(6);
     uint32_t em = NO_STOP;
 #pragma unroll
     for (int w = 0; w < NW; w++) em = sh.wmin[w] < em ? sh.wmin[w] : em;
@@ -495,7 +497,7 @@ __device__ __attribute__((always_inline)) inline void tb_round(
         // the next window must be in the ring before the round barrier
         const uint32_t nf = first + epos + (estep ? 1u : 0u);
         ld_until(L, sh, nf, nf + WIN, j1, pre, lane);
-        RL_PHASE(5);
+        RL_PHASE(7);
         return;
     }
 
@@ -533,7 +535,7 @@ __device__ __attribute__((always_inline)) inline void tb_round(
         sh.baseE[np] = E;
         sh.first[np] = first + epos;
     }
-    RL_PHASE(5);
+    RL_PHASE(7);
 #undef RL_PHASE
 }
 
@@ -545,7 +547,7 @@ __device__ __attribute__((always_inline)) inline void replay_tb_lanes(
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const bool loader = (tid >> 6) == (uint32_t)TB_NW;
     uint32_t nrounds = 0, niters = 0, par = 0;
-    uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     TbLoader L;
     L.next = j0 / 128u;
     L.issued = 0;
@@ -597,7 +599,7 @@ __device__ __attribute__((always_inline)) inline void replay_tb_lanes(
 #ifdef RL_STAMPS
     // every wave reports its own phase sums (16-cycle units), longest segment
     if ((tid & 63) == 0 && dbg)
-        for (int k = 0; k < 6; k++) atomicMax(&dbg[24 + 6 * (tid >> 6) + k], (uint32_t)(cyc[k] >> 4));
+        for (int k = 0; k < 8; k++) atomicMax(&dbg[24 + 8 * (tid >> 6) + k], (uint32_t)(cyc[k] >> 4));
 #endif
     if (tid == 0) {
         e->tok = tb_value(sh.baseD[par], sh.baseE[par], profile);

@@ -209,7 +209,7 @@ class Engine:
         lib.rl_engine_stats(self.h, C.byref(s))
         return s
 
-    def debug_words(self, n=72) -> np.ndarray:
+    def debug_words(self, n=88) -> np.ndarray:
         out = np.zeros(n, np.uint32)
         lib.rl_engine_debug_words(self.h, _ptr(out), n)
         return out

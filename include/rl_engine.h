@@ -126,7 +126,7 @@ int rl_engine_stats(rl_engine* e, rl_stats* out);
  * 2 segments, 3 replay.  Requires rl_engine_set_timing(e, 1). */
 int rl_engine_set_timing(rl_engine* e, int on);
 int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint64_t* batches);
-/* diagnostic: the last batch's replay debug counters (up to 72 words; layout in rl_engine.hip CTRL_DBG) */
+/* diagnostic: the last batch's replay debug counters (up to 88 words; layout in rl_engine.hip CTRL_DBG) */
 int rl_engine_debug_words(rl_engine* e, uint32_t* out, size_t n);
 
 int rl_last_error(rl_engine* e, char* buf, size_t len);

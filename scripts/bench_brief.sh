@@ -14,5 +14,5 @@ w = r.get("wave_phase_cycles", [])
 if any(w):
     n = max(1, r["stamp_cycles_longest_segment"][6])
     for k in range(8):
-        print("  wave", k, "cycles/round per phase", [round(x / n) for x in w[6 * k:6 * k + 6]])
+        print("  wave", k, "cycles/round per phase", [round(x / n) for x in w[8 * k:8 * k + 8]])
 PY
