@@ -209,8 +209,8 @@ def main():
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
-                          "coop_ends": [int(x) for x in st.coop_ends],
-                          "wave_phase_cycles": [int(x) * 16 for x in dbgw[24:88]]},
+                          "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
+                          "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21])},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
                                                     (stage_ms / nbat).tolist())},
     }

@@ -136,9 +136,11 @@ namespace {
 constexpr int NSTAGES = 4;
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
-constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2] k_replay queue heads [3] k_tb_coop queue
-constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] iterations [2] max rounds [3..6] round ends
-                                               // [8..19] timers / stamps [24..87] per-wave stamps
+constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2,3] k_replay queue heads
+                                               // [4] k_tb_chain queue [5] huge count
+constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iterations [2] max rounds
+                                               // [3..6] round ends (full, stop, partial, first window)
+                                               // [8..19] timers [20] exact tiles [21] serial steps
 constexpr uint32_t CTRL_DBGN = 88;
 constexpr uint32_t CTRL_WORDS = CTRL_DBG + CTRL_DBGN;
 
@@ -176,6 +178,7 @@ struct rl_engine {
     uint32_t max_tiles = 0;
     uint32_t *d_sk0 = nullptr, *d_sk1 = nullptr, *d_sv0 = nullptr, *d_sv1 = nullptr;
     SegRec* d_heavy = nullptr;
+    SegRec* d_huge = nullptr;
     // requests and results in sorted order (k_permute / k_unpermute)
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
@@ -184,13 +187,14 @@ struct rl_engine {
     double* o_tok = nullptr;
     // token-bucket precomputation (k_permute)
     double *q_add = nullptr, *q_lq = nullptr;
-    uint64_t* q_nc = nullptr;
-    TbRuns runs{};            // cooperative replay's committed runs (by start position)
+    double* q_th = nullptr;
+    TbRuns runs{};            // the chain's committed runs (by start position)
     int64_t* q_when = nullptr;
     SegRec* d_light = nullptr;
     int replay_grid = 2048;
-    int coop_grid = 512;        // k_tb_coop blocks (one per CU fits its LDS)
+    int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
     uint32_t heavy_min = 32;   // segments this long replay cooperatively
+    uint32_t huge_min = 4096;  // token-bucket segments this long are dequeued first
     uint32_t* d_zero = nullptr;  // ctrl words + look-back status (memset per batch)
     size_t zero_bytes = 0;
     uint32_t* d_ctrl = nullptr;
@@ -233,10 +237,11 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_win);
     (void)hipFree(e->d_sk0); (void)hipFree(e->d_sk1); (void)hipFree(e->d_sv0); (void)hipFree(e->d_sv1);
     (void)hipFree(e->d_heavy);
+    (void)hipFree(e->d_huge);
     (void)hipFree(e->p_ts); (void)hipFree(e->p_n); (void)hipFree(e->p_sms); (void)hipFree(e->p_cfg);
     (void)hipFree(e->o_dec); (void)hipFree(e->o_rem); (void)hipFree(e->o_retry); (void)hipFree(e->o_reset);
     (void)hipFree(e->o_tok);
-    (void)hipFree(e->q_add); (void)hipFree(e->q_nc);
+    (void)hipFree(e->q_add); (void)hipFree(e->q_th);
     (void)hipFree(e->runs.len); (void)hipFree(e->runs.E); (void)hipFree(e->runs.D0); (void)hipFree(e->runs.D1); (void)hipFree(e->q_lq); (void)hipFree(e->q_when);
     (void)hipFree(e->d_light);
     (void)hipFree(e->d_zero);
@@ -269,7 +274,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
     size_t M = e->max_batch;
-    // q_add and q_nc carry 128 elements of slack: the replay's loader wave
+    // q_add and q_th carry 128 elements of slack: the chain's loader wave
     // reads them in aligned 128-element chunks that may end past the batch
     e->cfg_cap = 64;
     bool ok = true;
@@ -281,6 +286,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_sv0, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_sv1, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_heavy, sizeof(SegRec) * M) == hipSuccess;
+    ok &= hipMalloc(&e->d_huge, sizeof(SegRec) * (M / 4096 + 1)) == hipSuccess;
     ok &= hipMalloc(&e->p_ts, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->p_n, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->p_sms, 8 * M) == hipSuccess;
@@ -291,7 +297,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->o_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->o_tok, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->q_add, 8 * (M + 128)) == hipSuccess;
-    ok &= hipMalloc(&e->q_nc, 8 * (M + 128)) == hipSuccess;
+    ok &= hipMalloc(&e->q_th, 8 * (M + 128)) == hipSuccess;
     ok &= hipMalloc(&e->runs.len, 2 * M) == hipSuccess;
     ok &= hipMalloc(&e->runs.E, 2 * M) == hipSuccess;
     ok &= hipMalloc(&e->runs.D0, 8 * M) == hipSuccess;
@@ -322,6 +328,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (hipMemsetAsync(e->runs.len, 0, 2 * M, e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
+    if (const char* v = getenv("RL_HUGE_MIN")) e->huge_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_REPLAY_GRID")) e->replay_grid = atoi(v);
     if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
     e->stats.sort_bits = e->sort_bits;
@@ -411,35 +418,37 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     // sorted keys/values are now in kin/vin
     uint32_t* segctr = e->d_ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
-    k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->heavy_min, e->d_heavy, segctr, e->d_light,
-                                      segctr + 1);
+    k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
+                                      std::max(e->huge_min, e->heavy_min), e->d_heavy, segctr, e->d_light,
+                                      segctr + 1, e->d_huge, segctr + 5);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset, e->o_tok};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
     // the TB reset time is state-independent: k_permute writes it straight
     // into the sorted result buffer
-    TbPre pre{e->q_add, e->q_nc, e->o_reset, e->q_lq, e->q_when};
+    TbPre pre{e->q_add, e->q_th, e->o_reset, e->q_lq, e->q_when};
     k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_tb, e->d_cfg, e->profile, a, ps,
                                     pre);
     if (e->timing) (void)hipEventRecord(ev[3], s);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = e->d_ctrl + CTRL_DBG;
     if (ncfg <= (uint32_t)MAX_LCFG) {
-        k_tb_coop<true><<<e->coop_grid, TB_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, segctr + 4, e->win_base, e->d_tb,
-                                                          e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
-                                                          e->runs);
+        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, e->d_huge, segctr + 5, e->d_heavy, segctr,
+                                                           segctr + 4, e->win_base, e->d_tb, e->d_cfg, ncfg,
+                                                           e->profile, ps, pre, e->d_eflags, dbg, e->runs);
         k_replay<true><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                               segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
                                                               ncfg, e->profile, ps, pre, e->d_eflags, dbg);
     } else {
-        k_tb_coop<false><<<e->coop_grid, TB_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, segctr + 4, e->win_base, e->d_tb,
-                                                           e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
-                                                           e->runs);
+        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, e->d_huge, segctr + 5, e->d_heavy, segctr,
+                                                            segctr + 4, e->win_base, e->d_tb, e->d_cfg, ncfg,
+                                                            e->profile, ps, pre, e->d_eflags, dbg, e->runs);
         k_replay<false><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
                                                                segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
                                                                ncfg, e->profile, ps, pre, e->d_eflags, dbg);
     }
-    k_tb_expand<<<pgrid, 256, 0, s>>>(m, e->runs, e->d_cfg, e->profile, ps, pre, e->d_eflags);
+    k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, 0, s>>>(
+        m, e->runs, e->profile, ps, pre, e->d_eflags);
     k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     if (e->timing) {
         (void)hipEventRecord(ev[4], s);

@@ -34,8 +34,8 @@ struct ReqArgs {
 struct TbPre {
     double* add;       // elapsed * refill_rate (tokenbucket.go:36-37); NaN when HMGET finds
                        // no live key (tokenbucket.go:31-34: tokens = capacity, add = 0)
-    uint64_t* nc;      // (cfg << 32) | n for the cooperative replay's loader; n field 0
-                       // when n >= 2^31 (the exact path then reads ReqArgs::n)
+    double* th;        // min(capacity, float64(n)): the script step allows or clamps
+                       // exactly when capacity-free sum >= th (tokenbucket.go:38-43)
     int64_t* reset;    // calculateResetTime (tokenbucket.go:161-165); aliases the sorted
                        // result buffer, so TB replay never rewrites reset_at
     double* lq;        // tostring(now) as stored in last_refill (tokenbucket.go:48)
@@ -183,16 +183,6 @@ __device__ inline double tb_value(int64_t D, int32_t E, int32_t profile) {
     return ldexp((double)D, E);
 }
 
-// Diagnostic build only (-DRL_STAMPS): per-phase shader-clock sums of the
-// cooperative replay, read back through the debug counters; never in the
-// product build (stamps serialize the phases they measure).
-#ifdef RL_STAMPS
-#define RL_STAMP(v) do { __builtin_amdgcn_sched_barrier(0); (v) = __builtin_amdgcn_s_memtime(); \
-                         __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_sched_barrier(0); } while (0)
-#else
-#define RL_STAMP(v) do { } while (0)
-#endif
-
 // Barrier for LDS hand-offs only.  __syncthreads() is a workgroup-scope
 // fence on gfx950 and waits for every outstanding global store (vmcnt(0));
 // the replay rounds scatter results to HBM between barriers and must not wait
@@ -324,25 +314,29 @@ struct SegRec {
 
 }  // namespace rl
 
-#include "rl_tb_lanes.h"
+#include "rl_tb_chain.h"
 
 namespace rl {
 
 
-// segment heads -> (start, length), split into heavy (cooperative) and light
-// (one thread each) work lists.  One tile of SEG_TILE sorted positions per
-// block; list slots are reserved with ONE global atomic per list per block
-// (a single contended word sustains only ~88 atomics/us on MI355X).
+// segment heads -> (start, length), split into work lists: huge token-bucket
+// segments (the chain replays these first: longest-first keeps one hot key
+// from starting last), heavy (cooperative for token bucket, serial for the
+// windows) and light (one thread each).  One tile of SEG_TILE sorted
+// positions per block; list slots are reserved with ONE global atomic per
+// list per block (a single contended word sustains only ~88 atomics/us on
+// MI355X).
 constexpr int SEG_ITEMS = 16;
 constexpr int SEG_TILE = 256 * SEG_ITEMS;
 
 __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ sk, uint32_t m,
-                                                  uint32_t invalid_key, uint32_t heavy_min, SegRec* heavy,
-                                                  uint32_t* nheavy, SegRec* light, uint32_t* nlight) {
-    __shared__ uint32_t s_cnt[2], s_base[2];
+                                                  uint32_t invalid_key, uint32_t win_base, uint32_t heavy_min,
+                                                  uint32_t huge_min, SegRec* heavy, uint32_t* nheavy, SegRec* light,
+                                                  uint32_t* nlight, SegRec* huge, uint32_t* nhuge) {
+    __shared__ uint32_t s_cnt[3], s_base[3];
     const uint32_t tid = threadIdx.x;
     for (uint32_t tile = blockIdx.x; tile * SEG_TILE < m; tile += gridDim.x) {
-        if (tid < 2) s_cnt[tid] = 0;
+        if (tid < 3) s_cnt[tid] = 0;
         __syncthreads();
         SegRec rec[SEG_ITEMS];
         uint32_t slot[SEG_ITEMS];
@@ -356,19 +350,21 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
             if (!head) continue;
             uint32_t len = seg_end(sk, m, i, k) - i;
             rec[j] = SegRec{i, len};
-            uint32_t which = len >= heavy_min ? 0u : 1u;
-            slot[j] = (which << 31) | atomicAdd(&s_cnt[which], 1u);
+            uint32_t which = len >= heavy_min ? (len >= huge_min && k < win_base ? 2u : 0u) : 1u;
+            slot[j] = (which << 30) | atomicAdd(&s_cnt[which], 1u);
         }
         __syncthreads();
         if (tid == 0) s_base[0] = s_cnt[0] ? atomicAdd(nheavy, s_cnt[0]) : 0u;
         if (tid == 1) s_base[1] = s_cnt[1] ? atomicAdd(nlight, s_cnt[1]) : 0u;
+        if (tid == 2) s_base[2] = s_cnt[2] ? atomicAdd(nhuge, s_cnt[2]) : 0u;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < SEG_ITEMS; j++) {
             if (slot[j] == 0xffffffffu) continue;
-            uint32_t which = slot[j] >> 31, off = slot[j] & 0x7fffffffu;
+            uint32_t which = slot[j] >> 30, off = slot[j] & 0x3fffffffu;
             if (which == 0) heavy[s_base[0] + off] = rec[j];
-            else light[s_base[1] + off] = rec[j];
+            else if (which == 1) light[s_base[1] + off] = rec[j];
+            else huge[s_base[2] + off] = rec[j];
         }
         __syncthreads();
     }
@@ -411,7 +407,7 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
         const bool alive = key_alive(prev_when, sms, profile);
         pre.add[j] = alive ? (now - prev_last) * C.rate : __builtin_nan("");
         const int64_t nv = in.n[i];
-        pre.nc[j] = ((uint64_t)c << 32) | (nv < (1LL << 31) ? (uint32_t)nv : 0u);
+        pre.th[j] = fmin(C.limit_d, (double)nv);
         pre.reset[j] = tb_reset_at(now, C);
         pre.lq[j] = lua_tostring_roundtrip(now, profile);
         pre.when[j] = expire_when(C.ttl_tb, sms);
@@ -460,7 +456,7 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
 }
 
 // Work-queue replay of everything except heavy token-bucket segments (those
-// run in k_tb_coop): heavy window segments one per block (serial, thread 0),
+// run in k_tb_chain): heavy window segments one per block (serial, thread 0),
 // then the light list, one segment per thread.
 constexpr int REPLAY_BLOCK = 256;
 

@@ -101,6 +101,48 @@ def test_hot_keys_long_segments(rl):
         run_both(rl, profile, configs, split((key, ts, n, cfg, None), [100_000, 100_000]))
 
 
+def _chain_trace(kind, seed, m=120_000):
+    """Few keys, long token-bucket segments, chosen to drive the chain through
+    its regimes: deep denial (near steps, decade crossings), frequent allows
+    (regime exits every few steps), sub-nanosecond gaps and huge n."""
+    rng = np.random.default_rng(seed)
+    if kind == "deny":        # one hot key: 8 us gaps against 20 tokens / 12 s
+        key = np.zeros(m, np.uint64)
+        gaps = np.rint(rng.exponential(8_000, m))
+        n = np.ones(m, np.int64)
+    elif kind == "allow":     # 3 keys, 10/s with 40 ms gaps: allows mixed with denials
+        key = rng.integers(0, 3, m).astype(np.uint64)
+        gaps = np.rint(rng.exponential(15_000_000, m))
+        n = rng.choice([1, 1, 1, 2], m).astype(np.int64)
+    else:                     # "mixed": bursts of zero gaps, rare long gaps, huge n
+        key = rng.integers(0, 2, m).astype(np.uint64)
+        gaps = rng.choice([0, 1, 1000, 90_000, 400_000_000], m, p=[0.2, 0.2, 0.3, 0.29, 0.01])
+        n = rng.choice([1, 1, 1, 2, 7], m).astype(np.int64)
+        n[rng.random(m) < 0.001] = 1 << 62
+    ts = T0 + np.cumsum(gaps).astype(np.int64)
+    cfg = (key % 3).astype(np.uint32)
+    return key, ts, n, cfg, None
+
+
+@pytest.mark.parametrize("profile", [0, 1])
+@pytest.mark.parametrize("kind", ["deny", "allow", "mixed"])
+def test_chain_regimes(rl, profile, kind):
+    configs = [(1, 20, 12 * NS), (1, 10, NS), (1, 3, 300_000_000)]
+    seed = {"deny": 1, "allow": 2, "mixed": 3}[kind] * 10 + profile
+    run_both(rl, profile, configs, split(_chain_trace(kind, seed), [50_000, 70_000]))
+
+
+def test_single_hot_key_full_batch(rl):
+    # the bench's diagnostic workload: one key carries the whole 1M batch
+    g = traces.TokenBucketZipf(nkeys=1, batch=1_000_000)
+    run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 10, win=1 << 10)
+
+
+def test_zipf15_full_batch(rl):
+    g = traces.TokenBucketZipf(s=1.5, batch=1_000_000)
+    run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 21, win=1 << 10)
+
+
 # --- BASELINE configs at full batch size ----------------------------------------
 
 def test_config1_tb_zipf_full_batches(rl):
