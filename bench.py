@@ -210,7 +210,9 @@ def main():
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
                           "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
-                          "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21])},
+                          "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
+                          "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
+                          "hw_id": [hex(int(x)) for x in dbgw[40:45]]},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
                                                     (stage_ms / nbat).tolist())},
     }

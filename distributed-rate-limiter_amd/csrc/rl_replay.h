@@ -250,7 +250,11 @@ __device__ inline TbEval tb_eval(int mode, int64_t Dpred, int32_t E, double P, d
     if (mode == QM_DEC) {
         if (at > 0.0 && at * P < 1.4e14) {
             v.Dact = rlq::round_scaled_P(at, P);
-            v.inrange = v.Dact >= 10000000000000LL && v.Dact < 100000000000000LL;
+            // the exact at*P must not be below 1e13: [1e13 - 0.5, 1e13) rounds to
+            // 1e13 here, while %.14g keeps 14 digits of the decade below
+            const double p = at * P, err = __builtin_fma(at, P, -p);
+            const bool ge_lo = p > 1e13 || (p == 1e13 && err >= 0.0);
+            v.inrange = ge_lo && v.Dact < 100000000000000LL;
         }
     } else if (mode == QM_BIN) {
         const double w = at * P;                                         // exact scaling

@@ -84,6 +84,7 @@ struct ChTile {
     int64_t S;          // nominal sum of the tile's increments r
     double ymin;        // min over steps of (th * P * CH_YSCALE - inclusive nominal prefix)
     double cmax, cmin;  // max / min inclusive nominal prefix
+    double dmax;        // the near band assumed every state of the tile is <= dmax
     uint32_t ev;        // first expired / huge step (tile-relative) or NO_STOP
     uint32_t nc;        // near steps (> CH_NE: list overflow)
 };
@@ -96,6 +97,7 @@ struct ChState {
     uint32_t ccnt;
     uint32_t pfirst;    // producers' window start (== cfirst + ccnt when ccnt > 0)
     uint32_t pbuf, cbuf;
+    uint32_t hot;       // diagnostics: segment of >= 65536 requests
 };
 
 struct ChainShared {
@@ -105,17 +107,16 @@ struct ChainShared {
     double ne_pred[2][CH_NP][CH_NE];   // tile-relative nominal predecessor of each near step
     double ne_add[2][CH_NP][CH_NE];
     double ne_th[2][CH_NP][CH_NE];
+    uint16_t ne_rank[2][CH_NP][64];    // near steps of the tile before each producer lane
     int32_t ne_off[CH_NP * CH_NE];     // chain: resolved offset after each near step
     ChState st[2];
 };
 
 __device__ inline double ring_add(const ChainShared& sh, uint32_t p) {
-    const double2 g = sh.r_add[ring_slot(p >> 1)];
-    return (p & 1u) ? g.y : g.x;
+    return reinterpret_cast<const double*>(&sh.r_add[ring_slot(p >> 1)])[p & 1u];
 }
 __device__ inline double ring_th(const ChainShared& sh, uint32_t p) {
-    const double2 g = sh.r_th[ring_slot(p >> 1)];
-    return (p & 1u) ? g.y : g.x;
+    return reinterpret_cast<const double*>(&sh.r_th[ring_slot(p >> 1)])[p & 1u];
 }
 
 // ---------------------------------------------------------------------------
@@ -216,14 +217,19 @@ __device__ __attribute__((always_inline)) inline void ld_until(TbLoader& L, Chai
 // ---------------------------------------------------------------------------
 // exact step in a fast mode
 // ---------------------------------------------------------------------------
-// RNE(x * P) as an exact integer-valued double (x*P < 2^52), P = 10^k exact
-__device__ inline double round_scaled_Pd(double x, double P) {
+// RNE(x * P) as an exact integer-valued double (x*P < 2^52), P = 10^k exact;
+// ge_lo: the exact x*P >= 1e13, i.e. x is not below the decade (a value in
+// [1e13 - 0.5, 1e13) units rounds to 1e13 here but %.14g formats it with 14
+// digits of the decade below)
+__device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
     const double p = x * P;
     const double err = __builtin_fma(x, P, -p);       // x*P == p + err exactly
+    ge_lo = (p > (double)DEC_LO) | ((p == (double)DEC_LO) & (err >= 0.0));
     const double d0 = floor(p);
     const double f = p - d0;                          // exact
     const bool odd = d0 * 0.5 != floor(d0 * 0.5);
-    const bool up = (f > 0.5) || (f == 0.5 && ((err > 0.0) || (err == 0.0 && odd)));
+    // bitwise, not short-circuit: no branches in the chain's hot loop
+    const bool up = (f > 0.5) | ((f == 0.5) & ((err > 0.0) | ((err == 0.0) & odd)));
     return up ? d0 + 1.0 : d0;
 }
 
@@ -240,8 +246,9 @@ __device__ inline double tb_step_d(double Dpred, double P, double R, double add,
     tokens = sum;
     double Dn;
     if (MODE == QM_DEC) {
-        Dn = round_scaled_Pd(sum, P);                               // %.14g of a positive sum
-        if (!(Dn >= (double)DEC_LO && Dn < (double)DEC_HI)) Dn = __builtin_nan("");
+        bool ge_lo;
+        Dn = round_scaled_Pd(sum, P, ge_lo);                        // %.14g of a positive sum
+        if (!(ge_lo & (Dn < (double)DEC_HI))) Dn = __builtin_nan("");
     } else {
         Dn = sum * P;                                               // exact scaling
         if (!(Dn >= (double)BIN_LO && Dn < (double)BIN_HI && Dn == floor(Dn))) Dn = __builtin_nan("");
@@ -288,16 +295,18 @@ struct GlobSrc {
 
 // Exact replay of [p, p + len) (len <= CH_TILE) from the exact stored digits
 // D0 by one wave: lane l steps requests [p + 8l, p + 8l + 8) from a guessed
-// start; the guesses are refined by an exclusive scan of every lane's actual
-// change until the first lane whose start changed lies past the first regime
-// exit (by induction over lanes, every start up to there is then exact).
-// Returns the relative position of the first step that leaves the regime
-// (len if none) and in Dend the exact digits before it (after the span).
+// start (nominal prefix + goff, the caller's guess of the lane's offset); the
+// guesses are refined by an exclusive scan of every lane's actual change until
+// the first lane whose start changed lies past the first regime exit (by
+// induction over lanes, every start up to there is then exact).  Returns the
+// relative position of the first step that leaves the regime (len if none)
+// and in Dend the exact digits before it (after the span).
 // OUT: writes tokens and DENIED for every in-regime step.
 template <int MODE, bool OUT, typename Src>
 __device__ __attribute__((always_inline)) inline uint32_t exact_span(const Src& src, uint32_t p, uint32_t len,
-                                                                     int64_t D0, double P, double R, int64_t& Dend,
-                                                                     const ReqArgs& a, uint32_t& iters) {
+                                                                     int64_t D0, int32_t goff, double P, double R,
+                                                                     int64_t& Dend, const ReqArgs& a,
+                                                                     uint32_t& iters) {
     constexpr int K = CH_K;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t off = lane * K;
@@ -313,7 +322,7 @@ __device__ __attribute__((always_inline)) inline uint32_t exact_span(const Src& 
         if (fabs(pr) < 0x1p49) S += (int64_t)rint(pr);     // NaN / huge: a regime exit anyway
     }
     const int64_t incl = wave_incl_scan_i64(S);
-    int64_t st = D0 + incl - S;
+    int64_t st = D0 + incl - S + (lane ? goff : 0);
     const uint32_t last = len ? (len - 1) / K : 0u;
     for (;;) {
         double D = (double)st, Db = 0.0;
@@ -358,10 +367,13 @@ __device__ __attribute__((always_inline)) inline uint32_t exact_span(const Src& 
 // producers
 // ---------------------------------------------------------------------------
 // Summary of tile t of the window [pfirst, pfirst + pcnt) at scale P, into
-// tile[buf][t] and its near list.  State-free.
+// tile[buf][t], its near list and per-lane near ranks.  State-free except for
+// dmax, an estimated bound on the window's states that narrows the near band
+// (|delta| <= (|D| + |D'|) 2^-53); the chain checks the bound per tile.
 template <int MODE>
 __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh, uint32_t buf, uint32_t t,
-                                                                uint32_t pfirst, uint32_t pcnt, double P) {
+                                                                uint32_t pfirst, uint32_t pcnt, double P,
+                                                                double dmax) {
     constexpr int K = CH_K;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t toff = t * CH_TILE;
@@ -369,56 +381,34 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     const uint32_t myoff = toff + lane * K;
     const uint32_t nv = myoff < pcnt ? ((pcnt - myoff) < (uint32_t)K ? (pcnt - myoff) : (uint32_t)K) : 0u;
     const uint32_t i0 = pfirst + myoff;
-
-    // my positions [i0, i0 + K): K/2 granules, one more when i0 is odd
-    // (pfirst is block-uniform, so is the parity)
-    double add[K], th[K];
-    {
-        double ga[K + 2], gt[K + 2];
-        const uint32_t g0 = i0 >> 1;
-#pragma unroll
-        for (int j = 0; j < K / 2 + 1; j++) {
-            if (j < K / 2 || (i0 & 1u)) {
-                const double2 x = sh.r_add[ring_slot(g0 + j)];
-                const double2 y = sh.r_th[ring_slot(g0 + j)];
-                ga[2 * j] = x.x; ga[2 * j + 1] = x.y;
-                gt[2 * j] = y.x; gt[2 * j + 1] = y.y;
-            } else {
-                ga[2 * j] = ga[2 * j + 1] = 0.0;
-                gt[2 * j] = gt[2 * j + 1] = 0.0;
-            }
-        }
-        const uint32_t o = i0 & 1u;
-#pragma unroll
-        for (int q = 0; q < K; q++) {
-            const bool v = (uint32_t)q < nv;
-            add[q] = v ? (o ? ga[q + 1] : ga[q]) : 0.0;
-            th[q] = v ? (o ? gt[q + 1] : gt[q]) : __builtin_inf();
-        }
-    }
-    double cum = 0.0, cb[K];
-    double ymin = __builtin_inf(), cmax = -__builtin_inf(), cmin = __builtin_inf();
+    const double lim = 0.5 - (2.0 * dmax * 0x1.0000001p-53 + 0x1p-40);
+    const double PY = P * CH_YSCALE;
+    double add[K], th[K], cb[K];
+    double cum = 0.0, ymin = __builtin_inf(), cmax = -__builtin_inf(), cmin = __builtin_inf();
     uint32_t nearm = 0, evq = NO_STOP;
 #pragma unroll
     for (int q = 0; q < K; q++) {
-        const double a = add[q];
+        const bool v = (uint32_t)q < nv;
+        const double a = v ? ring_add(sh, i0 + q) : 0.0;
+        const double h = ring_th(sh, i0 + q);
+        add[q] = a;
+        th[q] = h;
         cb[q] = cum;
-        double pr = a * P;
-        double rr = rint(pr);
-        const bool ev = !(fabs(pr) < 0x1p49);                  // NaN (expired key) or huge
-        if (ev && evq == NO_STOP) evq = q;
-        if (ev) { pr = 0.0; rr = 0.0; }
+        const double pr = a * P;
+        const bool ok = fabs(pr) < 0x1p49;                 // else NaN (expired key) or huge: a stop
+        if (!ok && evq == NO_STOP) evq = q;
+        const double rr = rint(pr);
         if (MODE == QM_DEC) {
-            const double err = ev ? 0.0 : __builtin_fma(a, P, -pr);    // a*P == pr + err exactly
-            if (fabs((pr - rr) + err) > 0.5 - TAU_DEC) nearm |= 1u << q;
-        } else if (fabs(pr - rr) == 0.5) {                              // exact tie: parity decides
+            const double fr = (pr - rr) + __builtin_fma(a, P, -pr);   // a*P - rr, one rounding
+            if (ok && fabs(fr) > lim) nearm |= 1u << q;
+        } else if (ok && fabs(pr - rr) == 0.5) {                     // exact tie: parity decides
             nearm |= 1u << q;
         }
-        cum += rr;                                                      // exact: |cum| < 2^52
-        if ((uint32_t)q < nv) {
+        cum += ok ? rr : 0.0;                                         // exact: |cum| < 2^52
+        if (v) {
             cmax = fmax(cmax, cum);
             cmin = fmin(cmin, cum);
-            ymin = fmin(ymin, th[q] * P * CH_YSCALE - cum);
+            ymin = fmin(ymin, h * PY - cum);
         }
     }
     const int64_t Si = (int64_t)cum;
@@ -430,7 +420,8 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     const uint32_t ev_t = wave_min_u32(evq != NO_STOP ? lane * K + evq : NO_STOP);
     const uint32_t ncnt = (uint32_t)__popc(nearm);
     const uint32_t ninc = wave_scan_u32(ncnt, 0u, [](uint32_t x, uint32_t y) { return x + y; });
-    {
+    sh.ne_rank[buf][t][lane] = (uint16_t)(ninc - ncnt);
+    if (nearm) {
         uint32_t k = ninc - ncnt;
 #pragma unroll
         for (int q = 0; q < K; q++) {
@@ -450,6 +441,7 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
         T.ymin = ymin_t;
         T.cmax = cmax_t;
         T.cmin = cmin_t;
+        T.dmax = dmax;
         T.ev = ev_t;
         T.nc = ninc;
     }
@@ -460,20 +452,20 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
 // ---------------------------------------------------------------------------
 enum : uint32_t { CH_FULL = 0, CH_STOP = 1, CH_PARTIAL = 2 };
 
+// Diagnostic build only (-DRL_STAMPS): shader-clock sums per wave role and
+// phase for segments of >= 65536 requests, added into dbg[24..39].
+#ifdef RL_STAMPS
+#define CH_T(v) do { __builtin_amdgcn_sched_barrier(0); (v) = __builtin_amdgcn_s_memtime(); \
+                     __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define CH_T(v) do { } while (0)
+#endif
+
 struct ChOutcome {
     uint32_t kind;
     uint32_t q;        // FULL: window end; STOP: the exiting step; PARTIAL: end of the committed part
     int64_t D;         // exact stored digits before position q
 };
-
-__device__ inline void record_run(const TbRuns& runs, uint32_t pos, uint32_t len, int32_t E, int64_t D0, int64_t D1) {
-    if ((threadIdx.x & 63) == 0 && len) {
-        runs.len[pos] = (uint16_t)len;
-        runs.E[pos] = (int16_t)E;
-        runs.D0[pos] = D0;
-        runs.D1[pos] = D1;
-    }
-}
 
 // Resolve the chain window of state s (its tiles are in tile[s.cbuf]).
 template <int MODE>
@@ -481,6 +473,10 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                                                                      double R, const ReqArgs& a, const TbRuns& runs,
                                                                      uint32_t& iters, uint32_t* dbg) {
     const uint32_t lane = threadIdx.x & 63;
+#ifdef RL_STAMPS
+    const uint64_t t_in = __builtin_amdgcn_s_memtime();
+    const uint32_t it_in = iters;
+#endif
     const uint32_t cb = s.cbuf;
     const uint32_t nt = (s.ccnt + CH_TILE - 1) / CH_TILE;
     const double LO = MODE == QM_DEC ? (double)DEC_LO : (double)BIN_LO;
@@ -525,9 +521,9 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
 #pragma unroll
             for (int u = 1; u < CH_NP; u++) t += g >= NPF[u] ? 1u : 0u;
             const uint32_t k = v ? g - pick(NPF, t) : 0u;
-            const double pn = v ? (double)(s.D + pick(TS, t)) + sh.ne_pred[cb][t][k] : 0.0;
-            const double ad = v ? sh.ne_add[cb][t][k] : 0.0;
-            const double th = v ? sh.ne_th[cb][t][k] : __builtin_inf();
+            const double pn = (double)(s.D + pick(TS, t)) + sh.ne_pred[cb][t][k];
+            const double ad = sh.ne_add[cb][t][k];
+            const double th = sh.ne_th[cb][t][k];
             const double r = rint(ad * P);
             int32_t est = 0, flip = 0;
             uint32_t stop_lane = 64;
@@ -556,56 +552,90 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
         }
         __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ne_off visible to this wave
     }
+    const uint32_t nres = nstop < ne ? nstop : ne;      // ne_off[0, nres) are exact
+#ifdef RL_STAMPS
+    if (dbg && lane == 0 && s.hot) {
+        atomicAdd(&dbg[36], (uint32_t)((__builtin_amdgcn_s_memtime() - t_in) >> 4));
+        atomicAdd(&dbg[37], ne);
+        atomicAdd(&dbg[38], iters - it_in);
+    }
+#endif
 
-    // Tile walk: commit tiles whose bounds exclude a regime exit; replay the
-    // others exactly.
-    ChOutcome o;
-    o.kind = CH_FULL;
-    int64_t Dcur = s.D;        // exact digits at the current tile start
-    int32_t off = 0;           // offset (exact - nominal) at the current tile start
-    for (uint32_t t = 0; t < nt; t++) {
-        const ChTile T = sh.tile[cb][t];
-        const uint32_t pos = s.cfirst + t * CH_TILE;
-        const uint32_t len = (s.ccnt - t * CH_TILE) < CH_TILE ? (s.ccnt - t * CH_TILE) : CH_TILE;
-        const uint32_t npf1 = pick(NPF, t + 1);
-        const bool nst_in = nstop != NO_STOP && nstop < npf1;
-        const bool forced = t >= ovt || nst_in || T.ev != NO_STOP;
-        const int32_t off_out = (!forced && T.nc) ? sh.ne_off[npf1 - 1] : off;
-        const double Dt = (double)Dcur, nc = (double)T.nc;
-        const bool cand = forced || !(Dt + nc + T.cmax < HI) || !(Dt - nc + T.cmin >= LO) ||
-                          !(Dt + nc + 3.0 < T.ymin);
-        if (!cand) {
-            const int64_t D1 = Dcur + T.S + (off_out - off);
-            record_run(runs, pos, len, s.E, Dcur, D1);
-            Dcur = D1;
-            off = off_out;
-            continue;
-        }
-        int64_t Dq = 0;
-        const uint32_t brk = exact_span<MODE, false>(RingSrc{sh}, pos, len, Dcur, P, R, Dq, a, iters);
-        if (dbg && lane == 0) atomicAdd(&dbg[20], 1u);
-        record_run(runs, pos, brk, s.E, Dcur, Dq);
-        if (brk < len) {
-            o.kind = CH_STOP;
-            o.q = pos + brk;
-            o.D = Dq;
-            return o;
-        }
-        const bool agree = Dq == Dcur + T.S + (off_out - off);
-        Dcur = Dq;
-        off = off_out;
-        if (forced || !agree) {
-            if (t + 1 < nt) {
-                o.kind = CH_PARTIAL;
-                o.q = pos + len;
-                o.D = Dcur;
+    // Tile checks, one lane per tile: a tile whose bounds exclude a regime
+    // exit is committed as a run; the first other one is replayed exactly.
+    const bool tv = lane < nt;
+    const uint32_t tl = tv ? lane : 0u;
+    const ChTile T = sh.tile[cb][tl];
+    const uint32_t npf0 = pick(NPF, tl), npf1 = pick(NPF, tl + 1);
+    const uint32_t i0 = npf0 < nres ? npf0 : nres, i1 = npf1 < nres ? npf1 : nres;
+    const int32_t off_in = i0 ? sh.ne_off[i0 - 1] : 0;
+    const int32_t off_out = i1 ? sh.ne_off[i1 - 1] : 0;
+    const bool forced = tl >= ovt || (nstop != NO_STOP && nstop < npf1) || T.ev != NO_STOP;
+    const int64_t Dt = s.D + pick(TS, tl) + off_in;
+    const int64_t D1 = Dt + T.S + (off_out - off_in);
+    {
+        const double dD = (double)Dt, nc = (double)T.nc;
+        const bool cand = forced || !(dD + nc + T.cmax < HI) || !(dD - nc + T.cmin >= LO + 1.0) ||
+                          !(dD + nc + 3.0 < T.ymin) || !(dD + nc + fmax(T.cmax, 0.0) <= T.dmax);
+        const uint64_t candm = __ballot(tv && cand);
+        uint32_t lo = 0;                                   // tiles [lo, c) commit now
+        uint32_t c = first_lane(candm);
+        const uint32_t pos = s.cfirst + tl * CH_TILE;
+        const uint32_t len = (s.ccnt - tl * CH_TILE) < CH_TILE ? (s.ccnt - tl * CH_TILE) : CH_TILE;
+        for (;;) {
+            if (tv && lane >= lo && lane < c) {
+                runs.len[pos] = (uint16_t)len;
+                runs.E[pos] = (int16_t)s.E;
+                runs.D0[pos] = Dt;
+                runs.D1[pos] = D1;
+            }
+            ChOutcome o;
+            if (c >= nt) {
+                o.kind = CH_FULL;
+                o.q = s.cfirst + s.ccnt;
+                o.D = readlane_i64(D1, nt - 1);
                 return o;
             }
+            // exact replay of tile c from its exact start; lane guesses from
+            // the resolved near offsets
+            const uint32_t cpos = s.cfirst + c * CH_TILE;
+            const uint32_t clen = (s.ccnt - c * CH_TILE) < CH_TILE ? (s.ccnt - c * CH_TILE) : CH_TILE;
+            const int64_t Dc = readlane_i64(Dt, c);
+            const uint32_t cn0 = pick(NPF, c);
+            const int32_t cin = (int32_t)__builtin_amdgcn_readlane(off_in, (int)c);
+            int32_t goff = 0;
+            if (c < ovt) {
+                const uint32_t gi = cn0 + sh.ne_rank[cb][c][lane];
+                const uint32_t gc = gi < nres ? gi : nres;
+                goff = (gi > cn0 && gc) ? sh.ne_off[gc - 1] - cin : 0;
+            }
+            int64_t Dq = 0;
+            const uint32_t brk = exact_span<MODE, false>(RingSrc{sh}, cpos, clen, Dc, goff, P, R, Dq, a, iters);
+            if (dbg && lane == 0) atomicAdd(&dbg[20], 1u);
+            if (lane == 0 && brk) {
+                runs.len[cpos] = (uint16_t)brk;
+                runs.E[cpos] = (int16_t)s.E;
+                runs.D0[cpos] = Dc;
+                runs.D1[cpos] = Dq;
+            }
+            if (brk < clen) {
+                o.kind = CH_STOP;
+                o.q = cpos + brk;
+                o.D = Dq;
+                return o;
+            }
+            const bool agree = Dq == readlane_i64(D1, c);
+            const bool fc = __builtin_amdgcn_readlane((int)forced, (int)c) != 0;
+            if (fc || !agree) {
+                o.kind = c + 1 < nt ? CH_PARTIAL : CH_FULL;
+                o.q = cpos + clen;
+                o.D = Dq;
+                return o;
+            }
+            lo = c + 1;
+            c = first_lane(candm & ~((2ull << c) - 1ull));
         }
     }
-    o.q = s.cfirst + s.ccnt;
-    o.D = Dcur;
-    return o;
 }
 
 // Replay one heavy token-bucket segment [j0, j1) with the whole block.
@@ -616,6 +646,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                                                                 uint32_t* dbg, const TbRuns& runs) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t nrounds = 0, iters = 0, par = 0, nserial = 0;
+    uint64_t cyc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0;
+    (void)t0; (void)t1;
     TbLoader L;
     L.next = j0 / 128u;
     L.issued = 0;
@@ -630,6 +662,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         s0.pfirst = j0;
         s0.pbuf = 0;
         s0.cbuf = 1;
+        s0.hot = j1 - j0 >= 65536u;
         sh.st[0] = s0;
     }
     if (wave == (uint32_t)CH_LOADER) ld_until(L, sh, j0, j0 + 2 * CH_W, j1, pre, lane);
@@ -642,17 +675,36 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         double P = 1.0, R = 1.0;
         if (s.mode != QM_NONE) mode_scale(s.mode, s.E, P, R);
         nrounds++;
+        CH_T(t0);
         if (wave >= 1 && wave <= (uint32_t)CH_NP) {
             if (pcnt) {
-                if (s.mode == QM_DEC) ch_produce<QM_DEC>(sh, s.pbuf, wave - 1, s.pfirst, pcnt, P);
-                else ch_produce<QM_BIN>(sh, s.pbuf, wave - 1, s.pfirst, pcnt, P);
+                if (s.mode == QM_DEC) {
+                    // bound on the window's states: the chain window's base plus
+                    // 2.25x its nominal growth (the chain verifies it per tile)
+                    double dmax = (double)DEC_HI;
+                    if (s.ccnt == CH_W) {
+                        int64_t G = 0;
+#pragma unroll
+                        for (int t = 0; t < CH_NP; t++) G += sh.tile[s.cbuf][t].S;
+                        dmax = fmin(dmax, (double)s.D + 2.25 * (double)(G > 0 ? G : 0) + 0x1p21);
+                    }
+                    ch_produce<QM_DEC>(sh, s.pbuf, wave - 1, s.pfirst, pcnt, P, dmax);
+                } else {
+                    ch_produce<QM_BIN>(sh, s.pbuf, wave - 1, s.pfirst, pcnt, P, (double)BIN_HI);
+                }
             }
+            __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            CH_T(t1);
+            cyc[0] += t1 - t0;
         } else if (wave == (uint32_t)CH_LOADER) {
             const uint32_t first = s.ccnt ? s.cfirst : s.pfirst;
             ld_until(L, sh, first, s.pfirst + 2 * CH_W, j1, pre, lane);
+            CH_T(t1);
+            cyc[0] += t1 - t0;
         } else {
             // ---- chain wave ----
             ChState nx;
+            nx.hot = s.hot;
             nx.pbuf = s.pbuf ^ 1u;
             nx.cbuf = s.pbuf;
             ChOutcome o{CH_PARTIAL, s.pfirst, s.D};
@@ -661,6 +713,9 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, R, a, runs, iters, dbg)
                                      : ch_resolve<QM_BIN>(sh, s, P, R, a, runs, iters, dbg);
                 if (dbg && lane == 0) atomicAdd(&dbg[3 + o.kind], 1u);
+                CH_T(t1);
+                cyc[o.kind == CH_FULL ? 0 : 1] += t1 - t0;
+                t0 = t1;
                 if (o.kind == CH_FULL) {
                     restart = false;
                     nx.D = o.D;                 // exact at s.pfirst
@@ -685,6 +740,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 int64_t D = o.D;
                 int32_t E = s.E;
                 int32_t mode = fast_mode(D, E, profile);
+                double Ps = 1.0, Rs = 1.0;
+                if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
                 const uint32_t lim = (j1 - s.pfirst) < CH_W ? j1 : s.pfirst + CH_W;   // resident in the ring
                 const uint32_t pq = q + lane;
                 const int64_t nvec = pq < j1 ? a.n[pq] : 1;
@@ -694,17 +751,26 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                     const bool alive = add == add;
                     const int64_t nn = readlane_i64(nvec, k);
                     const CfgDev& C = cfgs[(uint32_t)__builtin_amdgcn_readlane((int)cvec, (int)k)];
-                    const TbEval v = tb_eval(QM_NONE, D, E, 1.0, 1.0, alive, alive ? add : 0.0, C.limit_d,
+                    const TbEval v = tb_eval(mode, D, E, Ps, Rs, alive, alive ? add : 0.0, C.limit_d,
                                              (double)nn, profile);
                     if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
                     force = v.allowed || v.clamped || !alive;
-                    const TbQ nq = tb_quant(v.tokens, profile);
-                    D = nq.D;
-                    E = nq.E;
-                    mode = fast_mode(D, E, profile);
+                    if (mode != QM_NONE && v.inrange) {
+                        D = v.Dact;                     // same decade / binade (sign may flip)
+                        mode = fast_mode(D, E, profile);
+                    } else {
+                        const TbQ nq = tb_quant(v.tokens, profile);
+                        D = nq.D;
+                        E = nq.E;
+                        mode = fast_mode(D, E, profile);
+                        if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
+                    }
                     q++;
                     nserial++;
                 }
+                CH_T(t1);
+                cyc[2] += t1 - t0;
+                t0 = t1;
                 nx.D = D;
                 nx.E = E;
                 nx.mode = mode;
@@ -715,8 +781,21 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             if (lane == 0) sh.st[par ^ 1u] = nx;
         }
         par ^= 1u;
+        CH_T(t0);
         lds_barrier();
+        CH_T(t1);
+        cyc[3] += t1 - t0;
     }
+#ifdef RL_STAMPS
+    // dbg[24 + 4 * role + k]: role 0 chain (full / stop rounds, serial, barrier),
+    // 1 producer wave 1 (produce, -, -, barrier), 2 loader (load, -, -, barrier)
+    if (lane == 0 && dbg && j1 - j0 >= 65536u) {
+        dbg[40 + wave] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | ((32 - 1) << 11));   // HW_ID
+        const uint32_t role = wave == 0 ? 0u : wave == 1 ? 1u : wave == (uint32_t)CH_LOADER ? 2u : 3u;
+        if (role < 3)
+            for (int k = 0; k < 4; k++) atomicAdd(&dbg[24 + 4 * role + k], (uint32_t)(cyc[k] >> 4));
+    }
+#endif
     if (tid == 0) {
         const ChState s = sh.st[par];
         e->tok = tb_value(s.D, s.E, profile);
@@ -764,10 +843,10 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
             double P, R;
             if (profile == PROFILE_REDIS7) {
                 mode_scale(QM_DEC, E, P, R);
-                brk = exact_span<QM_DEC, true>(GlobSrc{pre.add, pre.th}, p, len, D0, P, R, Dend, a, iters);
+                brk = exact_span<QM_DEC, true>(GlobSrc{pre.add, pre.th}, p, len, D0, 0, P, R, Dend, a, iters);
             } else {
                 mode_scale(QM_BIN, E, P, R);
-                brk = exact_span<QM_BIN, true>(GlobSrc{pre.add, pre.th}, p, len, D0, P, R, Dend, a, iters);
+                brk = exact_span<QM_BIN, true>(GlobSrc{pre.add, pre.th}, p, len, D0, 0, P, R, Dend, a, iters);
             }
             if (lane == 0) {
                 if (brk != len || Dend != D1) atomicOr(eflags, EF_INTERNAL);
