@@ -136,8 +136,8 @@ namespace {
 constexpr int NSTAGES = 4;
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
-constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0] heavy count [1] light count [2,3] k_replay queue heads
-                                               // [4] k_tb_chain queue [5] huge count
+constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0..3] list counts (heavy TB, light, heavy window, huge TB)
+                                               // [4] chain queue [5] per-thread queue
 constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iterations [2] max rounds
                                                // [3..6] round ends (full, stop, partial, first window)
                                                // [8..19] timers [20] exact tiles [21] serial steps
@@ -179,6 +179,7 @@ struct rl_engine {
     uint32_t *d_sk0 = nullptr, *d_sk1 = nullptr, *d_sv0 = nullptr, *d_sv1 = nullptr;
     SegRec* d_heavy = nullptr;
     SegRec* d_huge = nullptr;
+    SegRec* d_wheavy = nullptr;
     // requests and results in sorted order (k_permute / k_unpermute)
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
@@ -191,7 +192,6 @@ struct rl_engine {
     TbRuns runs{};            // the chain's committed runs (by start position)
     int64_t* q_when = nullptr;
     SegRec* d_light = nullptr;
-    int replay_grid = 2048;
     int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
     uint32_t heavy_min = 32;   // segments this long replay cooperatively
     uint32_t huge_min = 4096;  // token-bucket segments this long are dequeued first
@@ -238,6 +238,7 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_sk0); (void)hipFree(e->d_sk1); (void)hipFree(e->d_sv0); (void)hipFree(e->d_sv1);
     (void)hipFree(e->d_heavy);
     (void)hipFree(e->d_huge);
+    (void)hipFree(e->d_wheavy);
     (void)hipFree(e->p_ts); (void)hipFree(e->p_n); (void)hipFree(e->p_sms); (void)hipFree(e->p_cfg);
     (void)hipFree(e->o_dec); (void)hipFree(e->o_rem); (void)hipFree(e->o_retry); (void)hipFree(e->o_reset);
     (void)hipFree(e->o_tok);
@@ -287,6 +288,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_sv1, 4 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_heavy, sizeof(SegRec) * M) == hipSuccess;
     ok &= hipMalloc(&e->d_huge, sizeof(SegRec) * (M / 4096 + 1)) == hipSuccess;
+    ok &= hipMalloc(&e->d_wheavy, sizeof(SegRec) * M) == hipSuccess;
     ok &= hipMalloc(&e->p_ts, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->p_n, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->p_sms, 8 * M) == hipSuccess;
@@ -329,7 +331,6 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_HUGE_MIN")) e->huge_min = (uint32_t)atoi(v);
-    if (const char* v = getenv("RL_REPLAY_GRID")) e->replay_grid = atoi(v);
     if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
@@ -418,9 +419,9 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     // sorted keys/values are now in kin/vin
     uint32_t* segctr = e->d_ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
+    const SegLists lists{{e->d_heavy, e->d_light, e->d_wheavy, e->d_huge}, segctr};
     k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
-                                      std::max(e->huge_min, e->heavy_min), e->d_heavy, segctr, e->d_light,
-                                      segctr + 1, e->d_huge, segctr + 5);
+                                      std::max(e->huge_min, e->heavy_min), lists);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset, e->o_tok};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
@@ -432,21 +433,14 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) 
     if (e->timing) (void)hipEventRecord(ev[3], s);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = e->d_ctrl + CTRL_DBG;
-    if (ncfg <= (uint32_t)MAX_LCFG) {
-        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, e->d_huge, segctr + 5, e->d_heavy, segctr,
-                                                           segctr + 4, e->win_base, e->d_tb, e->d_cfg, ncfg,
-                                                           e->profile, ps, pre, e->d_eflags, dbg, e->runs);
-        k_replay<true><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
-                                                              segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
-                                                              ncfg, e->profile, ps, pre, e->d_eflags, dbg);
-    } else {
-        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, e->d_huge, segctr + 5, e->d_heavy, segctr,
-                                                            segctr + 4, e->win_base, e->d_tb, e->d_cfg, ncfg,
-                                                            e->profile, ps, pre, e->d_eflags, dbg, e->runs);
-        k_replay<false><<<e->replay_grid, REPLAY_BLOCK, 0, s>>>(kin, e->d_heavy, segctr, e->d_light, segctr + 1,
-                                                               segctr + 2, e->win_base, e->d_tb, e->d_win, e->d_cfg,
-                                                               ncfg, e->profile, ps, pre, e->d_eflags, dbg);
-    }
+    if (ncfg <= (uint32_t)MAX_LCFG)
+        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
+                                                           e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
+                                                           e->runs);
+    else
+        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
+                                                            e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
+                                                            e->runs);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, 0, s>>>(
         m, e->runs, e->profile, ps, pre, e->d_eflags);
     k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
@@ -543,14 +537,14 @@ extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t 
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     if (!e || !out) return RL_EINVAL;
     (void)hipSetDevice(e->device);
-    uint32_t c[2] = {0, 0}, d[24] = {0};
+    uint32_t c[4] = {0, 0, 0, 0}, d[24] = {0};
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpy(c, e->d_ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
     HIPCHK(e, hipMemcpy(d, e->d_ctrl + CTRL_DBG, sizeof d, hipMemcpyDeviceToHost));
     for (int k = 0; k < 6; k++) e->stats.stamp_cycles[k] = ((uint64_t)d[8 + 2 * k + 1] << 32) | d[8 + 2 * k];
     e->stats.stamp_cycles[6] = d[2];   // max rounds of one segment
-    e->stats.last_heavy = c[0];
-    e->stats.last_segments = (uint64_t)c[0] + c[1];
+    e->stats.last_heavy = c[0] + c[3];                        // chain (token-bucket) segments
+    e->stats.last_segments = (uint64_t)c[0] + c[1] + c[2] + c[3];
     e->stats.last_coop_rounds = d[0];
     e->stats.last_coop_iters = d[1];
     for (int k = 0; k < 4; k++) e->stats.coop_ends[k] = d[3 + k];

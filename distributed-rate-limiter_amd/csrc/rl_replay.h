@@ -316,6 +316,12 @@ struct SegRec {
     uint32_t len;
 };
 
+// the segment work lists k_segments builds (see there)
+struct SegLists {
+    SegRec* list[4];
+    uint32_t* count;      // 4 counters
+};
+
 }  // namespace rl
 
 #include "rl_tb_chain.h"
@@ -323,24 +329,25 @@ struct SegRec {
 namespace rl {
 
 
-// segment heads -> (start, length), split into work lists: huge token-bucket
-// segments (the chain replays these first: longest-first keeps one hot key
-// from starting last), heavy (cooperative for token bucket, serial for the
-// windows) and light (one thread each).  One tile of SEG_TILE sorted
-// positions per block; list slots are reserved with ONE global atomic per
-// list per block (a single contended word sustains only ~88 atomics/us on
-// MI355X).
+// segment heads -> (start, length), split into work lists:
+//   [0] heavy token-bucket segments (the chain, k_tb_chain),
+//   [1] light segments of any algorithm (one thread each),
+//   [2] heavy window segments (one thread each, dequeued before the light ones),
+//   [3] huge token-bucket segments (the chain dequeues these first: longest-first
+//       keeps one hot key from starting last).
+// One tile of SEG_TILE sorted positions per block; list slots are reserved
+// with ONE global atomic per list per block (a single contended word sustains
+// only ~88 atomics/us on MI355X).
 constexpr int SEG_ITEMS = 16;
 constexpr int SEG_TILE = 256 * SEG_ITEMS;
 
 __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ sk, uint32_t m,
                                                   uint32_t invalid_key, uint32_t win_base, uint32_t heavy_min,
-                                                  uint32_t huge_min, SegRec* heavy, uint32_t* nheavy, SegRec* light,
-                                                  uint32_t* nlight, SegRec* huge, uint32_t* nhuge) {
-    __shared__ uint32_t s_cnt[3], s_base[3];
+                                                  uint32_t huge_min, SegLists L) {
+    __shared__ uint32_t s_cnt[4], s_base[4];
     const uint32_t tid = threadIdx.x;
     for (uint32_t tile = blockIdx.x; tile * SEG_TILE < m; tile += gridDim.x) {
-        if (tid < 3) s_cnt[tid] = 0;
+        if (tid < 4) s_cnt[tid] = 0;
         __syncthreads();
         SegRec rec[SEG_ITEMS];
         uint32_t slot[SEG_ITEMS];
@@ -354,21 +361,18 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
             if (!head) continue;
             uint32_t len = seg_end(sk, m, i, k) - i;
             rec[j] = SegRec{i, len};
-            uint32_t which = len >= heavy_min ? (len >= huge_min && k < win_base ? 2u : 0u) : 1u;
+            const bool tb = k < win_base;
+            const uint32_t which = len < heavy_min ? 1u : !tb ? 2u : len >= huge_min ? 3u : 0u;
             slot[j] = (which << 30) | atomicAdd(&s_cnt[which], 1u);
         }
         __syncthreads();
-        if (tid == 0) s_base[0] = s_cnt[0] ? atomicAdd(nheavy, s_cnt[0]) : 0u;
-        if (tid == 1) s_base[1] = s_cnt[1] ? atomicAdd(nlight, s_cnt[1]) : 0u;
-        if (tid == 2) s_base[2] = s_cnt[2] ? atomicAdd(nhuge, s_cnt[2]) : 0u;
+        if (tid < 4) s_base[tid] = s_cnt[tid] ? atomicAdd(&L.count[tid], s_cnt[tid]) : 0u;
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < SEG_ITEMS; j++) {
             if (slot[j] == 0xffffffffu) continue;
-            uint32_t which = slot[j] >> 30, off = slot[j] & 0x3fffffffu;
-            if (which == 0) heavy[s_base[0] + off] = rec[j];
-            else if (which == 1) light[s_base[1] + off] = rec[j];
-            else huge[s_base[2] + off] = rec[j];
+            const uint32_t which = slot[j] >> 30, off = slot[j] & 0x3fffffffu;
+            L.list[which][s_base[which] + off] = rec[j];
         }
         __syncthreads();
     }
@@ -457,56 +461,6 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
         out.reset[i] = sorted.reset[j];
         if (out.tok) out.tok[i] = tok;
     }
-}
-
-// Work-queue replay of everything except heavy token-bucket segments (those
-// run in k_tb_chain): heavy window segments one per block (serial, thread 0),
-// then the light list, one segment per thread.
-constexpr int REPLAY_BLOCK = 256;
-
-template <bool LCFG>
-__global__ __launch_bounds__(REPLAY_BLOCK) void k_replay(
-    const uint32_t* __restrict__ sk, const SegRec* __restrict__ heavy,
-    const uint32_t* __restrict__ nheavy_p, const SegRec* __restrict__ light,
-    const uint32_t* __restrict__ nlight_p, uint32_t* qctr, uint32_t win_base, TbEntry* tb, WinEntry* win,
-    const CfgDev* __restrict__ gcfgs, uint32_t ncfg, int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
-    uint32_t* dbg) {
-    __shared__ uint32_t s_u;
-    __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
-    if (LCFG) {
-        for (uint32_t c = threadIdx.x; c < ncfg; c += blockDim.x) s_cfg[c] = gcfgs[c];
-        __syncthreads();
-    }
-    const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
-    const uint32_t nheavy = *nheavy_p, nlight = *nlight_p;
-    // heavy window segments: 64 per grab, one per block (serial replay by thread 0)
-    for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
-        __syncthreads();
-        const uint32_t u = s_u;
-        __syncthreads();
-        if (u >= nheavy) break;
-        const SegRec sg = heavy[u];
-        const uint32_t k0 = sk[sg.j0];
-        if (k0 >= win_base && threadIdx.x == 0)
-            replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
-    }
-    const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)REPLAY_BLOCK);
-        __syncthreads();
-        const uint32_t u0 = s_u;
-        __syncthreads();
-        if (u0 >= nlight) break;
-        const uint32_t u = u0 + threadIdx.x;
-        if (u < nlight) {
-            const SegRec sg = light[u];
-            const uint32_t k0 = sk[sg.j0];
-            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre);
-            else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
-        }
-    }
-    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
 }
 
 }  // namespace rl

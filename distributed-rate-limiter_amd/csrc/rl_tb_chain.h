@@ -23,7 +23,7 @@
 // One block replays one segment with three wave roles, in lock-step rounds
 // separated by one LDS barrier:
 //   producers (CH_NP waves)  summarize the NEXT window of CH_W requests at the
-//       current decade: per 512-request tile the nominal sum of r, bounds of
+//       current decade: per tile (64 lanes x CH_K requests) the nominal sum of r, bounds of
 //       the nominal prefix (decade exit), of the allow/clamp slack, the first
 //       expired/huge step, and the tile's near steps compacted into an LDS
 //       list -- all state-free, so they run one window ahead of the chain;
@@ -53,14 +53,25 @@ constexpr int64_t BIN_LO = 1LL << 52, BIN_HI = 1LL << 53;
 constexpr uint32_t NO_STOP = 0xffffffffu;
 
 #ifndef RL_CH_NP
-#define RL_CH_NP 3
+#define RL_CH_NP 6
 #endif
-constexpr int CH_K = 8;                                // requests per producer lane
+#ifndef RL_CH_K
+#define RL_CH_K 4
+#endif
+constexpr int CH_K = RL_CH_K;                          // requests per producer lane
 constexpr int CH_NP = RL_CH_NP;                        // producer waves
 constexpr uint32_t CH_TILE = 64u * CH_K;               // requests per producer wave
 constexpr uint32_t CH_W = (uint32_t)CH_NP * CH_TILE;   // requests per window
 constexpr int CH_NE = 64;                              // near-list capacity per tile
-constexpr int CH_LOADER = CH_NP + 1;                   // wave 0 chain, 1..NP producers
+// Wave roles.  Waves of a block are dealt to the CU's four SIMDs round-robin
+// (wave w on SIMD (w + base) mod 4), so the chain (wave 0) shares its SIMD
+// with the mostly idle loader (wave 4) and the producers pair up on the
+// other three SIMDs.
+constexpr int CH_LOADER = 4;
+static_assert(CH_NP + 2 <= 16 && CH_NP >= 3, "wave roles");
+__device__ inline int ch_producer_index(uint32_t wave) {
+    return wave == 0 || wave == (uint32_t)CH_LOADER ? -1 : (int)wave - (wave < (uint32_t)CH_LOADER ? 1 : 2);
+}
 constexpr int CH_BLOCK = (CH_NP + 2) * 64;
 constexpr int CH_SERIAL = 64;                          // serial exact steps per round at most
 // conservative scale of the allow/clamp threshold th*P (covers the rounding of
@@ -294,7 +305,7 @@ struct GlobSrc {
 };
 
 // Exact replay of [p, p + len) (len <= CH_TILE) from the exact stored digits
-// D0 by one wave: lane l steps requests [p + 8l, p + 8l + 8) from a guessed
+// D0 by one wave: lane l steps requests [p + K l, p + K l + K) from a guessed
 // start (nominal prefix + goff, the caller's guess of the lane's offset); the
 // guesses are refined by an exclusive scan of every lane's actual change until
 // the first lane whose start changed lies past the first regime exit (by
@@ -676,7 +687,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         if (s.mode != QM_NONE) mode_scale(s.mode, s.E, P, R);
         nrounds++;
         CH_T(t0);
-        if (wave >= 1 && wave <= (uint32_t)CH_NP) {
+        if (ch_producer_index(wave) >= 0) {
             if (pcnt) {
                 if (s.mode == QM_DEC) {
                     // bound on the window's states: the chain window's base plus
@@ -688,9 +699,9 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                         for (int t = 0; t < CH_NP; t++) G += sh.tile[s.cbuf][t].S;
                         dmax = fmin(dmax, (double)s.D + 2.25 * (double)(G > 0 ? G : 0) + 0x1p21);
                     }
-                    ch_produce<QM_DEC>(sh, s.pbuf, wave - 1, s.pfirst, pcnt, P, dmax);
+                    ch_produce<QM_DEC>(sh, s.pbuf, ch_producer_index(wave), s.pfirst, pcnt, P, dmax);
                 } else {
-                    ch_produce<QM_BIN>(sh, s.pbuf, wave - 1, s.pfirst, pcnt, P, (double)BIN_HI);
+                    ch_produce<QM_BIN>(sh, s.pbuf, ch_producer_index(wave), s.pfirst, pcnt, P, (double)BIN_HI);
                 }
             }
             __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -813,7 +824,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
 
 // Outputs of the committed runs: one wave per run, exact_span with outputs
 // from the run's exact start state, checked against the state the chain
-// resolved at the run's end.  Waves scan the batch in 512-position blocks and
+// resolved at the run's end.  Waves scan the batch in CH_TILE-position blocks and
 // expand the runs that start in their block.
 __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int32_t profile, ReqArgs a, TbPre pre,
                                                    uint32_t* eflags) {
@@ -856,15 +867,13 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
     }
 }
 
-// Heavy token-bucket segments: one per block from a work queue, the huge list
-// (longest segments) first; window segments in the heavy list are k_replay's.
+// The replay kernel.  Phase 1: huge then heavy token-bucket segments, one per
+// block (the chain).  Phase 2, as blocks run out of chains (the hot keys'
+// blocks are still busy): heavy window segments, then light segments of any
+// algorithm, one per thread, serial (replay_*_serial).
 template <bool LCFG>
-__global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restrict__ sk,
-                                                       const SegRec* __restrict__ huge,
-                                                       const uint32_t* __restrict__ nhuge_p,
-                                                       const SegRec* __restrict__ heavy,
-                                                       const uint32_t* __restrict__ nheavy_p, uint32_t* qctr,
-                                                       uint32_t win_base, TbEntry* tb,
+__global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restrict__ sk, SegLists L, uint32_t* qctr,
+                                                       uint32_t win_base, TbEntry* tb, WinEntry* win,
                                                        const CfgDev* __restrict__ gcfgs, uint32_t ncfg,
                                                        int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
                                                        uint32_t* dbg, TbRuns runs) {
@@ -876,25 +885,35 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         __syncthreads();
     }
     const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
-    const uint32_t nhuge = *nhuge_p, nheavy = *nheavy_p;
+    const uint32_t nheavy = L.count[0], nlight = L.count[1], nwin = L.count[2], nhuge = L.count[3];
     for (;;) {
-        if (threadIdx.x == 0) {
-            uint32_t u;
-            do {   // huge first, then heavy; skip window segments (k_replay's)
-                u = atomicAdd(qctr, 1u);
-            } while (u >= nhuge && u - nhuge < nheavy && sk[heavy[u - nhuge].j0] >= win_base);
-            s_u = u;
-        }
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
         __syncthreads();
         const uint32_t u = s_u;
         __syncthreads();
         if (u >= nhuge + nheavy) break;
-        const SegRec sg = u < nhuge ? huge[u] : heavy[u - nhuge];
+        const SegRec sg = u < nhuge ? L.list[3][u] : L.list[0][u - nhuge];
         const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
         ch_segment<LCFG>(sh, &tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
         __syncthreads();
         if (threadIdx.x == 0 && dbg) atomicMax(&dbg[8], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seg));
     }
+    const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)CH_BLOCK);
+        __syncthreads();
+        const uint32_t u0 = s_u;
+        __syncthreads();
+        if (u0 >= nwin + nlight) break;
+        const uint32_t u = u0 + threadIdx.x;
+        if (u < nwin + nlight) {
+            const SegRec sg = u < nwin ? L.list[2][u] : L.list[1][u - nwin];
+            const uint32_t k0 = sk[sg.j0];
+            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre);
+            else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+        }
+    }
+    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
 }
 
 }  // namespace rl
