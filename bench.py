@@ -89,6 +89,7 @@ def main():
     ap.add_argument("--workload", default="tb_zipf", choices=sorted(WORKLOAD_DESC))
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
     args = ap.parse_args()
 
     import torch
@@ -127,7 +128,10 @@ def main():
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7,
                         tb_capacity=keyspace if need_tb else 1024,
                         win_capacity=keyspace if algs - {1} else 1024,
-                        max_batch=args.batch, device=local_rank)
+                        max_batch=args.batch, device=local_rank,
+                        # inputs are resident before the timed region: batch b+1's
+                        # hash/sort/permute overlaps batch b's replay
+                        flags=0 if args.no_pipeline else rl_amd.OPT_PIPELINE)
     for a, L, W in gen.configs:
         eng.register(a, L, W)
     m = args.batch
@@ -202,7 +206,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
         "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
-                   "profile": "redis7 (Lua %.14g state round trip)", "parallelism": f"key-shard x{world}"},
+                   "profile": "redis7 (Lua %.14g state round trip)", "parallelism": f"key-shard x{world}",
+                   "batches_in_flight": 1 if args.no_pipeline else 2},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_decision": bytes_per_dec},

@@ -83,13 +83,6 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
                 if (s == NO_SLOT) ef |= EF_TABLE_FULL; else slot = win_base + s;
             }
         }
-        if (slot == invalid_key) {
-            a.dec[i] = DEC_INVALID;
-            a.rem[i] = 0;
-            a.retry[i] = 0;
-            a.reset[i] = 0;
-            if (a.tok) a.tok[i] = 0.0;
-        }
         sk[i] = slot;
         for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
     }
@@ -157,10 +150,38 @@ int bitlen(uint64_t v) {
 
 }  // namespace
 
+// Per-batch device buffers.  Two sets: with RL_OPT_PIPELINE, batch b's front
+// half (probe, sort, segments, permute) runs on the engine's front stream
+// while batch b-1's back half (replay, expansion, unpermute) still runs on the
+// caller's stream; set b & 1 is reused by batch b+2 only after batch b's back
+// half (back_done).
+struct BatchSet {
+    uint32_t *sk0 = nullptr, *sk1 = nullptr, *sv0 = nullptr, *sv1 = nullptr;
+    SegRec* list[4] = {nullptr, nullptr, nullptr, nullptr};   // heavy TB, light, heavy window, huge TB
+    // requests and results in sorted order (k_permute / k_unpermute)
+    int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
+    uint32_t* p_cfg = nullptr;
+    uint8_t* o_dec = nullptr;
+    int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
+    double* o_tok = nullptr;
+    // token-bucket precomputation (k_permute)
+    double *q_add = nullptr, *q_th = nullptr, *q_lq = nullptr;
+    int64_t* q_when = nullptr;
+    TbRuns runs{};                // the chain's committed runs (by start position)
+    uint32_t* zero = nullptr;     // ctrl words + look-back status (memset per batch)
+    uint32_t* ctrl = nullptr;
+    uint32_t* status = nullptr;
+    hipEvent_t front_done = nullptr, back_done = nullptr;
+    bool used = false;
+};
+
 struct rl_engine {
     int device = 0;
     int32_t profile = PROFILE_REDIS7;
-    hipStream_t stream = nullptr;
+    uint32_t flags = 0;
+    hipStream_t stream = nullptr;     // the engine's stream (host API; device API without a stream)
+    hipStream_t front = nullptr;      // front halves
+    hipEvent_t ev_in = nullptr;       // inputs ready (non-pipelined device API, host API)
     std::string err;
 
     std::vector<CfgDev> h_cfg;
@@ -176,29 +197,14 @@ struct rl_engine {
 
     uint32_t max_batch = 0;
     uint32_t max_tiles = 0;
-    uint32_t *d_sk0 = nullptr, *d_sk1 = nullptr, *d_sv0 = nullptr, *d_sv1 = nullptr;
-    SegRec* d_heavy = nullptr;
-    SegRec* d_huge = nullptr;
-    SegRec* d_wheavy = nullptr;
-    // requests and results in sorted order (k_permute / k_unpermute)
-    int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
-    uint32_t* p_cfg = nullptr;
-    uint8_t* o_dec = nullptr;
-    int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
-    double* o_tok = nullptr;
-    // token-bucket precomputation (k_permute)
-    double *q_add = nullptr, *q_lq = nullptr;
-    double* q_th = nullptr;
-    TbRuns runs{};            // the chain's committed runs (by start position)
-    int64_t* q_when = nullptr;
-    SegRec* d_light = nullptr;
-    int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
-    uint32_t heavy_min = 32;   // segments this long replay cooperatively
-    uint32_t huge_min = 4096;  // token-bucket segments this long are dequeued first
-    uint32_t* d_zero = nullptr;  // ctrl words + look-back status (memset per batch)
+    BatchSet set[2];
+    int next_set = 0, last_set = 0;
     size_t zero_bytes = 0;
-    uint32_t* d_ctrl = nullptr;
-    uint32_t* d_status = nullptr;
+    int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
+    int probe_grid = 1024;      // k_probe blocks at most
+    int perm_grid = 1024;       // k_permute / k_unpermute blocks at most
+    uint32_t heavy_min = 32;    // segments this long replay cooperatively
+    uint32_t huge_min = 4096;   // token-bucket segments this long are dequeued first
     uint32_t* d_eflags = nullptr;
 
     // host-API staging (device side)
@@ -209,10 +215,11 @@ struct rl_engine {
     int64_t *d_rem = nullptr, *d_retry = nullptr, *d_reset = nullptr;
     double* d_tok = nullptr;
 
-    // timing
+    // timing: front start, after probe, after sort, after segments+permute
+    // (front stream); back start, back end (launch stream)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::array<hipEvent_t, NSTAGES + 1>> ev_pending;
+    std::vector<std::array<hipEvent_t, 6>> ev_pending;
     double stage_ms[NSTAGES] = {0, 0, 0, 0};
     uint64_t timed_batches = 0;
 
@@ -231,26 +238,80 @@ static int fail(rl_engine* e, int code, const std::string& msg) {
             return fail((e), RL_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_st)); \
     } while (0)
 
+static void free_set(BatchSet& B) {
+    (void)hipFree(B.sk0); (void)hipFree(B.sk1); (void)hipFree(B.sv0); (void)hipFree(B.sv1);
+    for (auto* l : B.list) (void)hipFree(l);
+    (void)hipFree(B.p_ts); (void)hipFree(B.p_n); (void)hipFree(B.p_sms); (void)hipFree(B.p_cfg);
+    (void)hipFree(B.o_dec); (void)hipFree(B.o_rem); (void)hipFree(B.o_retry); (void)hipFree(B.o_reset);
+    (void)hipFree(B.o_tok);
+    (void)hipFree(B.q_add); (void)hipFree(B.q_th); (void)hipFree(B.q_lq); (void)hipFree(B.q_when);
+    (void)hipFree(B.runs.len); (void)hipFree(B.runs.E); (void)hipFree(B.runs.D0); (void)hipFree(B.runs.D1);
+    (void)hipFree(B.zero);
+    if (B.front_done) (void)hipEventDestroy(B.front_done);
+    if (B.back_done) (void)hipEventDestroy(B.back_done);
+}
+
+static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes) {
+    bool ok = true;
+    ok &= hipMalloc(&B.sk0, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.sk1, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.sv0, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.sv1, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.list[0], sizeof(SegRec) * M) == hipSuccess;
+    ok &= hipMalloc(&B.list[1], sizeof(SegRec) * M) == hipSuccess;
+    ok &= hipMalloc(&B.list[2], sizeof(SegRec) * M) == hipSuccess;
+    ok &= hipMalloc(&B.list[3], sizeof(SegRec) * (M / 4096 + 1)) == hipSuccess;
+    ok &= hipMalloc(&B.p_ts, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.p_n, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
+    ok &= hipMalloc(&B.o_rem, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.o_retry, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.o_reset, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.o_tok, 8 * M) == hipSuccess;
+    // q_add and q_th carry 128 elements of slack: the chain's loader wave
+    // reads them in aligned 128-element chunks that may end past the batch
+    ok &= hipMalloc(&B.q_add, 8 * (M + 128)) == hipSuccess;
+    ok &= hipMalloc(&B.q_th, 8 * (M + 128)) == hipSuccess;
+    ok &= hipMalloc(&B.q_lq, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.q_when, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.runs.len, 2 * M) == hipSuccess;
+    ok &= hipMalloc(&B.runs.E, 2 * M) == hipSuccess;
+    ok &= hipMalloc(&B.runs.D0, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.runs.D1, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.zero, zero_bytes) == hipSuccess;
+    ok &= hipEventCreateWithFlags(&B.front_done, hipEventDisableTiming) == hipSuccess;
+    ok &= hipEventCreateWithFlags(&B.back_done, hipEventDisableTiming) == hipSuccess;
+    if (!ok) return false;
+    B.ctrl = B.zero;
+    B.status = B.zero + CTRL_WORDS;
+    // run lengths start at 0; k_tb_expand clears every one it consumes
+    return hipMemset(B.runs.len, 0, 2 * M) == hipSuccess;
+}
+
 static void free_all(rl_engine* e) {
     (void)hipFree(e->d_cfg);
     (void)hipFree(e->d_tb);
     (void)hipFree(e->d_win);
-    (void)hipFree(e->d_sk0); (void)hipFree(e->d_sk1); (void)hipFree(e->d_sv0); (void)hipFree(e->d_sv1);
-    (void)hipFree(e->d_heavy);
-    (void)hipFree(e->d_huge);
-    (void)hipFree(e->d_wheavy);
-    (void)hipFree(e->p_ts); (void)hipFree(e->p_n); (void)hipFree(e->p_sms); (void)hipFree(e->p_cfg);
-    (void)hipFree(e->o_dec); (void)hipFree(e->o_rem); (void)hipFree(e->o_retry); (void)hipFree(e->o_reset);
-    (void)hipFree(e->o_tok);
-    (void)hipFree(e->q_add); (void)hipFree(e->q_th);
-    (void)hipFree(e->runs.len); (void)hipFree(e->runs.E); (void)hipFree(e->runs.D0); (void)hipFree(e->runs.D1); (void)hipFree(e->q_lq); (void)hipFree(e->q_when);
-    (void)hipFree(e->d_light);
-    (void)hipFree(e->d_zero);
+    for (auto& B : e->set) free_set(B);
     (void)hipFree(e->d_eflags);
     (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
     (void)hipFree(e->d_dec); (void)hipFree(e->d_rem); (void)hipFree(e->d_retry); (void)hipFree(e->d_reset); (void)hipFree(e->d_tok);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+    if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    if (e->front) (void)hipStreamDestroy(e->front);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+}
+
+// every queued kernel of the engine has finished (the engine's streams and,
+// through the back_done events, any caller stream a batch was enqueued on)
+static int drain(rl_engine* e) {
+    HIPCHK(e, hipStreamSynchronize(e->front));
+    for (auto& B : e->set)
+        if (B.used) HIPCHK(e, hipEventSynchronize(B.back_done));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    return RL_OK;
 }
 
 extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
@@ -258,9 +319,11 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     *out = nullptr;
     if (o->profile != PROFILE_REDIS7 && o->profile != PROFILE_MINIREDIS) return RL_EINVAL;
     if (o->max_batch == 0 || o->max_batch > (1u << 28)) return RL_EINVAL;
+    if (o->flags & ~(uint32_t)RL_OPT_PIPELINE) return RL_EINVAL;
     rl_engine* e = new rl_engine();
     e->device = o->device;
     e->profile = o->profile;
+    e->flags = o->flags;
     e->tb_cap = pow2_at_least(std::max<uint64_t>(o->tb_capacity, 1024));
     e->win_cap = pow2_at_least(std::max<uint64_t>(o->win_capacity, 1024));
     if (e->tb_cap + e->win_cap >= (1ull << 31)) { delete e; return RL_EINVAL; }
@@ -274,41 +337,16 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     auto bail = [&](int code) { int r = code; free_all(e); delete e; return r; };
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
     size_t M = e->max_batch;
-    // q_add and q_th carry 128 elements of slack: the chain's loader wave
-    // reads them in aligned 128-element chunks that may end past the batch
     e->cfg_cap = 64;
+    e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
     bool ok = true;
     ok &= hipMalloc(&e->d_cfg, sizeof(CfgDev) * e->cfg_cap) == hipSuccess;
     ok &= hipMalloc(&e->d_tb, sizeof(TbEntry) * e->tb_cap) == hipSuccess;
     ok &= hipMalloc(&e->d_win, sizeof(WinEntry) * e->win_cap) == hipSuccess;
-    ok &= hipMalloc(&e->d_sk0, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_sk1, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_sv0, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_sv1, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_heavy, sizeof(SegRec) * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_huge, sizeof(SegRec) * (M / 4096 + 1)) == hipSuccess;
-    ok &= hipMalloc(&e->d_wheavy, sizeof(SegRec) * M) == hipSuccess;
-    ok &= hipMalloc(&e->p_ts, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->p_n, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->p_sms, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->p_cfg, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&e->o_dec, M) == hipSuccess;
-    ok &= hipMalloc(&e->o_rem, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->o_retry, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->o_reset, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->o_tok, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_add, 8 * (M + 128)) == hipSuccess;
-    ok &= hipMalloc(&e->q_th, 8 * (M + 128)) == hipSuccess;
-    ok &= hipMalloc(&e->runs.len, 2 * M) == hipSuccess;
-    ok &= hipMalloc(&e->runs.E, 2 * M) == hipSuccess;
-    ok &= hipMalloc(&e->runs.D0, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->runs.D1, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_lq, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->q_when, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&e->d_light, sizeof(SegRec) * M) == hipSuccess;
-    e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
-    ok &= hipMalloc(&e->d_zero, e->zero_bytes) == hipSuccess;
+    for (auto& B : e->set) ok = ok && alloc_set(B, M, e->zero_bytes);
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
     ok &= hipMalloc(&e->d_key, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_ts, 8 * M) == hipSuccess;
@@ -321,17 +359,16 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_tok, 8 * M) == hipSuccess;
     if (!ok) return bail(RL_ENOMEM);
-    e->d_ctrl = e->d_zero;
-    e->d_status = e->d_zero + CTRL_WORDS;
     k_init_tb<<<2048, 256, 0, e->stream>>>(e->d_tb, e->tb_cap);
     k_init_win<<<2048, 256, 0, e->stream>>>(e->d_win, e->win_cap);
     if (hipMemsetAsync(e->d_eflags, 0, 4, e->stream) != hipSuccess) return bail(RL_EDEVICE);
-    // run lengths start at 0; k_tb_expand clears every one it consumes
-    if (hipMemsetAsync(e->runs.len, 0, 2 * M, e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipDeviceSynchronize() != hipSuccess) return bail(RL_EDEVICE);
     if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_HUGE_MIN")) e->huge_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
+    if (const char* v = getenv("RL_PROBE_GRID")) e->probe_grid = atoi(v);
+    if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
     *out = e;
@@ -341,7 +378,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
 extern "C" int rl_engine_destroy(rl_engine* e) {
     if (!e) return RL_EINVAL;
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    (void)drain(e);
     free_all(e);
     delete e;
     return RL_OK;
@@ -358,6 +395,8 @@ extern "C" int rl_config_register(rl_engine* e, uint8_t alg, int64_t limit, int6
     if (window_ns > 365LL * 24 * 3600 * NS_PER_S) return fail(e, RL_EINVAL, "window too large");
     CfgDev c = make_cfg(alg, limit, window_ns);
     (void)hipSetDevice(e->device);
+    int r = drain(e);                  // queued batches read d_cfg
+    if (r != RL_OK) return r;
     if (e->h_cfg.size() == e->cfg_cap) {
         CfgDev* nd = nullptr;
         HIPCHK(e, hipMalloc(&nd, sizeof(CfgDev) * e->cfg_cap * 2));
@@ -386,68 +425,88 @@ static hipEvent_t take_event(rl_engine* e) {
     return ev;
 }
 
-// enqueue one launch sequence for m <= max_batch requests
-static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s) {
+// enqueue one batch of m <= max_batch requests: front half on e->front, back
+// half on s.  inputs_ready: the caller guarantees the input arrays are
+// complete now (RL_OPT_PIPELINE); otherwise the front half waits for s.
+static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, bool inputs_ready) {
     if (m == 0) return RL_OK;
-    std::array<hipEvent_t, NSTAGES + 1> ev{};
+    BatchSet& B = e->set[e->next_set];
+    e->last_set = e->next_set;
+    e->next_set ^= 1;
+    hipStream_t f = e->front;
+    if (!inputs_ready) {
+        HIPCHK(e, hipEventRecord(e->ev_in, s));
+        HIPCHK(e, hipStreamWaitEvent(f, e->ev_in, 0));
+    }
+    if (B.used) HIPCHK(e, hipStreamWaitEvent(f, B.back_done, 0));   // set reuse
+    std::array<hipEvent_t, 6> ev{};
     if (e->timing) {
         for (auto& x : ev) x = take_event(e);
-        (void)hipEventRecord(ev[0], s);
+        (void)hipEventRecord(ev[0], f);
     }
-    HIPCHK(e, hipMemsetAsync(e->d_zero, 0, e->zero_bytes, s));
-    uint32_t* ghist = e->d_ctrl + CTRL_HIST;
-    int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, 4096);
-    k_probe<<<probe_grid, PROBE_BLOCK, 0, s>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
+    HIPCHK(e, hipMemsetAsync(B.zero, 0, e->zero_bytes, f));
+    uint32_t* ghist = B.ctrl + CTRL_HIST;
+    // few enough blocks that the per-block histogram flush (3 x 256 global
+    // atomics per block on 768 shared words) stays cheap
+    int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, (uint32_t)e->probe_grid);
+    k_probe<<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
                                                 e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
-                                                e->win_base, e->invalid_key, e->d_sk0, ghist,
+                                                e->win_base, e->invalid_key, B.sk0, ghist,
                                                 e->sort_passes, a, e->d_eflags);
-    if (e->timing) (void)hipEventRecord(ev[1], s);
+    if (e->timing) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
-    uint32_t *kin = e->d_sk0, *vin = e->d_sv0, *kout = e->d_sk1, *vout = e->d_sv1;
+    uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
     for (int p = 0; p < e->sort_passes; p++) {
-        uint32_t* status = e->d_status + (size_t)p * e->max_tiles * RADIX;
+        uint32_t* status = B.status + (size_t)p * e->max_tiles * RADIX;
         if (p == 0)
-            k_sort_pass<true><<<tiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
-                                                           status, e->d_ctrl + CTRL_TILE + p, e->d_eflags);
+            k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
+                                                           status, B.ctrl + CTRL_TILE + p, e->d_eflags);
         else
-            k_sort_pass<false><<<tiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
-                                                            status, e->d_ctrl + CTRL_TILE + p, e->d_eflags);
+            k_sort_pass<false><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
+                                                            status, B.ctrl + CTRL_TILE + p, e->d_eflags);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    if (e->timing) (void)hipEventRecord(ev[2], s);
+    if (e->timing) (void)hipEventRecord(ev[2], f);
     // sorted keys/values are now in kin/vin
-    uint32_t* segctr = e->d_ctrl + CTRL_NSEG;
+    uint32_t* segctr = B.ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
-    const SegLists lists{{e->d_heavy, e->d_light, e->d_wheavy, e->d_huge}, segctr};
-    k_segments<<<sgrid, 256, 0, s>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
+    const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr};
+    k_segments<<<sgrid, 256, 0, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
                                       std::max(e->huge_min, e->heavy_min), lists);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
-    ReqArgs ps{nullptr, e->p_ts, e->p_n, e->p_cfg, e->p_sms, e->o_dec, e->o_rem, e->o_retry, e->o_reset, e->o_tok};
-    int pgrid = (int)std::min<uint32_t>((m + 255) / 256, 4096);
+    ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, B.p_sms, B.o_dec, B.o_rem, B.o_retry, B.o_reset, B.o_tok};
+    int pgrid = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
     // the TB reset time is state-independent: k_permute writes it straight
     // into the sorted result buffer
-    TbPre pre{e->q_add, e->q_th, e->o_reset, e->q_lq, e->q_when};
-    k_permute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_tb, e->d_cfg, e->profile, a, ps,
-                                    pre);
-    if (e->timing) (void)hipEventRecord(ev[3], s);
+    TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
+    k_permute<<<pgrid, 256, 0, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, a, ps, pre);
+    if (e->timing) (void)hipEventRecord(ev[3], f);
+    HIPCHK(e, hipEventRecord(B.front_done, f));
+
+    // back half: the replay needs this batch's front half and the previous
+    // batch's back half (stream order on s) for the table state
+    HIPCHK(e, hipStreamWaitEvent(s, B.front_done, 0));
+    if (e->timing) (void)hipEventRecord(ev[4], s);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
-    uint32_t* dbg = e->d_ctrl + CTRL_DBG;
+    uint32_t* dbg = B.ctrl + CTRL_DBG;
     if (ncfg <= (uint32_t)MAX_LCFG)
         k_tb_chain<true><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
                                                            e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
-                                                           e->runs);
+                                                           B.runs);
     else
         k_tb_chain<false><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
                                                             e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
-                                                            e->runs);
+                                                            B.runs);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, 0, s>>>(
-        m, e->runs, e->profile, ps, pre, e->d_eflags);
+        m, B.runs, e->profile, ps, pre, e->d_eflags);
     k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     if (e->timing) {
-        (void)hipEventRecord(ev[4], s);
+        (void)hipEventRecord(ev[5], s);
         e->ev_pending.push_back(ev);
     }
+    HIPCHK(e, hipEventRecord(B.back_done, s));
+    B.used = true;
     HIPCHK(e, hipGetLastError());
     e->stats.batches++;
     e->stats.decisions += m;
@@ -465,8 +524,8 @@ static int check_flags(rl_engine* e, uint32_t f) {
 extern "C" int rl_engine_sync(rl_engine* e) {
     if (!e) return RL_EINVAL;
     (void)hipSetDevice(e->device);
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipDeviceSynchronize());
+    int r = drain(e);
+    if (r != RL_OK) return r;
     uint32_t f = 0;
     HIPCHK(e, hipMemcpy(&f, e->d_eflags, 4, hipMemcpyDeviceToHost));
     HIPCHK(e, hipMemset(e->d_eflags, 0, 4));
@@ -486,7 +545,7 @@ extern "C" int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* ke
         ReqArgs a{key_id + off, ts_ns + off, n + off, cfg_id + off, server_ms ? server_ms + off : nullptr,
                   decision + off, remaining + off, retry_after_ns + off, reset_at_ns + off,
                   tokens ? tokens + off : nullptr};
-        int r = run_batch(e, c, a, s);
+        int r = run_batch(e, c, a, s, (e->flags & RL_OPT_PIPELINE) != 0);
         if (r != RL_OK) return r;
     }
     return RL_OK;
@@ -510,7 +569,7 @@ extern "C" int rl_decide_batch(rl_engine* e, size_t m, const uint64_t* key_id, c
         if (server_ms) HIPCHK(e, hipMemcpyAsync(e->d_sms, server_ms + off, 8 * (size_t)c, hipMemcpyHostToDevice, s));
         ReqArgs a{e->d_key, e->d_ts, e->d_n, e->d_cfgid, server_ms ? e->d_sms : nullptr,
                   e->d_dec, e->d_rem, e->d_retry, e->d_reset, tokens ? e->d_tok : nullptr};
-        int r = run_batch(e, c, a, s);
+        int r = run_batch(e, c, a, s, false);
         if (r != RL_OK) return r;
         HIPCHK(e, hipMemcpyAsync(decision + off, e->d_dec, c, hipMemcpyDeviceToHost, s));
         HIPCHK(e, hipMemcpyAsync(remaining + off, e->d_rem, 8 * (size_t)c, hipMemcpyDeviceToHost, s));
@@ -527,6 +586,8 @@ extern "C" int rl_decide_batch(rl_engine* e, size_t m, const uint64_t* key_id, c
 extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns) {
     if (!e || cfg_id >= e->h_cfg.size() || key_id == EMPTY_KEY) return RL_EINVAL;
     (void)hipSetDevice(e->device);
+    int r = drain(e);
+    if (r != RL_OK) return r;
     k_reset<<<1, 1, 0, e->stream>>>(key_id, ts_ns, e->d_cfg, cfg_id, e->d_tb, e->tb_cap - 1, e->d_win,
                                      e->win_cap - 1);
     HIPCHK(e, hipGetLastError());
@@ -538,9 +599,11 @@ extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     if (!e || !out) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     uint32_t c[4] = {0, 0, 0, 0}, d[24] = {0};
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipMemcpy(c, e->d_ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
-    HIPCHK(e, hipMemcpy(d, e->d_ctrl + CTRL_DBG, sizeof d, hipMemcpyDeviceToHost));
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    const uint32_t* ctrl = e->set[e->last_set].ctrl;
+    HIPCHK(e, hipMemcpy(c, ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(d, ctrl + CTRL_DBG, sizeof d, hipMemcpyDeviceToHost));
     for (int k = 0; k < 6; k++) e->stats.stamp_cycles[k] = ((uint64_t)d[8 + 2 * k + 1] << 32) | d[8 + 2 * k];
     e->stats.stamp_cycles[6] = d[2];   // max rounds of one segment
     e->stats.last_heavy = c[0] + c[3];                        // chain (token-bucket) segments
@@ -562,10 +625,11 @@ extern "C" int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint
     if (!e) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     for (auto& ev : e->ev_pending) {
-        HIPCHK(e, hipEventSynchronize(ev[NSTAGES]));
+        HIPCHK(e, hipEventSynchronize(ev[5]));
+        static const int from[NSTAGES] = {0, 1, 2, 4}, to[NSTAGES] = {1, 2, 3, 5};
         for (int k = 0; k < NSTAGES; k++) {
             float t = 0;
-            HIPCHK(e, hipEventElapsedTime(&t, ev[k], ev[k + 1]));
+            HIPCHK(e, hipEventElapsedTime(&t, ev[from[k]], ev[to[k]]));
             e->stage_ms[k] += t;
         }
         e->timed_batches++;
@@ -584,8 +648,9 @@ extern "C" int rl_engine_debug_words(rl_engine* e, uint32_t* out, size_t n) {
     if (!e || !out) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     if (n > CTRL_DBGN) n = CTRL_DBGN;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipMemcpy(out, e->d_ctrl + CTRL_DBG, 4 * n, hipMemcpyDeviceToHost));
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    HIPCHK(e, hipMemcpy(out, e->set[e->last_set].ctrl + CTRL_DBG, 4 * n, hipMemcpyDeviceToHost));
     return RL_OK;
 }
 

@@ -33,7 +33,9 @@ struct ReqArgs {
 // previous sorted position (or, for a segment head, the table entry).
 struct TbPre {
     double* add;       // elapsed * refill_rate (tokenbucket.go:36-37); NaN when HMGET finds
-                       // no live key (tokenbucket.go:31-34: tokens = capacity, add = 0)
+                       // no live key (tokenbucket.go:31-34: tokens = capacity, add = 0).
+                       // A segment head's add depends on the table state, so the
+                       // replay computes it (tb_head_add); k_permute fills the rest
     double* th;        // min(capacity, float64(n)): the script step allows or clamps
                        // exactly when capacity-free sum >= th (tokenbucket.go:38-43)
     int64_t* reset;    // calculateResetTime (tokenbucket.go:161-165); aliases the sorted
@@ -120,11 +122,21 @@ __device__ inline Out tb_chain_step(double& tok, bool alive, double add, int64_t
     return o;
 }
 
+// add of a segment head: its predecessor is the table entry (the state after
+// the previous batch), read at replay time
+__device__ inline double tb_head_add(const TbEntry* e, uint32_t j0, const CfgDev* cfgs, int32_t profile,
+                                     const ReqArgs& a) {
+    const CfgDev& C = cfgs[a.cfg[j0]];
+    const double now = (double)a.ts[j0] / 1e9;
+    return key_alive(e->when, a.sms[j0], profile) ? (now - e->last) * C.rate : __builtin_nan("");
+}
+
 __device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
                                         int32_t profile, const ReqArgs& a, const TbPre& pre) {
     double tok = e->tok;
+    const double add0 = tb_head_add(e, j0, cfgs, profile, a);
     for (uint32_t j = j0; j < j1; j++) {
-        const double add = pre.add[j];
+        const double add = j == j0 ? add0 : pre.add[j];
         const bool alive = add == add;
         Out o = tb_chain_step(tok, alive, alive ? add : 0.0, a.n[j], 0, cfgs[a.cfg[j]], profile);
         write_out_tb(a, j, o.decision, o.tokens);
@@ -383,8 +395,8 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
 // plus the token-bucket precomputation (TbPre)
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
-                                                 const TbEntry* __restrict__ tb, const CfgDev* __restrict__ cfgs,
-                                                 int32_t profile, ReqArgs in, ReqArgs out, TbPre pre) {
+                                                 const CfgDev* __restrict__ cfgs, int32_t profile, ReqArgs in,
+                                                 ReqArgs out, TbPre pre) {
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
         const uint32_t k0 = sk[j];
         if (k0 == invalid_key) continue;
@@ -400,20 +412,16 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
         if (k0 >= win_base) continue;
         const CfgDev& C = cfgs[c];
         const double now = (double)t / 1e9;
-        double prev_last;
-        int64_t prev_when;
-        if (j == 0 || sk[j - 1] != k0) {
-            prev_last = tb[k0].last;
-            prev_when = tb[k0].when;
-        } else {
+        // state-free: a head's add needs the table (tb_head_add, at replay)
+        // and the table is still being updated by the previous batch
+        if (j > 0 && sk[j - 1] == k0) {
             const uint32_t ip = sv[j - 1];
             const int64_t tp = in.ts[ip];
             const int64_t smsp = in.sms ? in.sms[ip] : floor_div(tp, 1000000LL);
-            prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
-            prev_when = expire_when(cfgs[in.cfg[ip]].ttl_tb, smsp);
+            const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
+            const int64_t prev_when = expire_when(cfgs[in.cfg[ip]].ttl_tb, smsp);
+            pre.add[j] = key_alive(prev_when, sms, profile) ? (now - prev_last) * C.rate : __builtin_nan("");
         }
-        const bool alive = key_alive(prev_when, sms, profile);
-        pre.add[j] = alive ? (now - prev_last) * C.rate : __builtin_nan("");
         const int64_t nv = in.n[i];
         pre.th[j] = fmin(C.limit_d, (double)nv);
         pre.reset[j] = tb_reset_at(now, C);
@@ -444,8 +452,15 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
                                                    const CfgDev* __restrict__ cfgs, ReqArgs sorted, ReqArgs out) {
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
         const uint32_t k0 = sk[j];
-        if (k0 == invalid_key) continue;
         const uint32_t i = sv[j];
+        if (k0 == invalid_key) {   // rejected by k_probe (n <= 0, unknown config or key, table full)
+            out.dec[i] = DEC_INVALID;
+            out.rem[i] = 0;
+            out.retry[i] = 0;
+            out.reset[i] = 0;
+            if (out.tok) out.tok[i] = 0.0;
+            continue;
+        }
         const uint8_t dec = sorted.dec[j];
         const double tok = sorted.tok[j];
         int64_t rem, retry;

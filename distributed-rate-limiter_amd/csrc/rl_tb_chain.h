@@ -676,7 +676,16 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         s0.hot = j1 - j0 >= 65536u;
         sh.st[0] = s0;
     }
-    if (wave == (uint32_t)CH_LOADER) ld_until(L, sh, j0, j0 + 2 * CH_W, j1, pre, lane);
+    if (wave == (uint32_t)CH_LOADER) {
+        ld_until(L, sh, j0, j0 + 2 * CH_W, j1, pre, lane);
+        // the head's add comes from the table entry: into the ring and HBM
+        // (k_tb_expand reads it there)
+        if (lane == 0) {
+            const double add0 = tb_head_add(e, j0, cfgs, profile, a);
+            pre.add[j0] = add0;
+            reinterpret_cast<double*>(&sh.r_add[ring_slot(j0 >> 1)])[j0 & 1u] = add0;
+        }
+    }
     lds_barrier();
     for (;;) {
         const ChState s = sh.st[par];

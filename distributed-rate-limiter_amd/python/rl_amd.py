@@ -136,12 +136,16 @@ class Decisions:
     tokens: np.ndarray | None
 
 
+# rl_opts.flags (include/rl_engine.h)
+OPT_PIPELINE = 1
+
+
 class Engine:
     """rl_engine: the batched decision engine on one GPU."""
 
     def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
-                 max_batch=1 << 20, device=0):
-        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, 0)
+                 max_batch=1 << 20, device=0, flags=0):
+        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, flags)
         h = vp()
         rc = lib.rl_engine_create(C.byref(o), C.byref(h))
         if rc != RL_OK:

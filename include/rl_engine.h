@@ -61,8 +61,15 @@ typedef struct rl_opts {
     uint64_t tb_capacity;   /* token-bucket table slots; rounded up to a power of 2 */
     uint64_t win_capacity;  /* window-counter table slots; rounded up to a power of 2 */
     uint32_t max_batch;     /* largest batch one launch sequence handles (<= 2^28) */
-    uint32_t flags;         /* reserved, 0 */
+    uint32_t flags;         /* RL_OPT_* */
 } rl_opts;
+
+/* rl_opts.flags: the device-API input arrays of every rl_decide_batch_device
+ * call are complete when the call is made (not produced by work still queued
+ * on `stream`).  The engine then overlaps a batch's grouping (hash, sort,
+ * permute) with the previous batch's replay, on a second internal stream;
+ * results are identical. */
+#define RL_OPT_PIPELINE 1u
 
 typedef struct rl_stats {
     uint64_t batches;

@@ -222,3 +222,43 @@ def test_deterministic_repeat(rl):
     for a, b in zip(*outs):
         assert np.array_equal(a.decision, b.decision)
         assert np.array_equal(a.tokens.view(np.uint64), b.tokens.view(np.uint64))
+
+
+# --- device API, pipelined batches -----------------------------------------------
+
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_device_api_batches_in_flight(rl, pipeline):
+    """Several device-API batches enqueued back to back (with RL_OPT_PIPELINE
+    the engine overlaps batch b+1's grouping with batch b's replay); every
+    batch's results must equal the oracle's."""
+    import torch
+    configs = CONFIG_SETS["mixed"]
+    tr = random_trace(91, 80_000, 400, configs, big_n=True)
+    sizes = [20_000, 15_000, 25_000, 20_000]
+    eng = rl.Engine(profile=0, tb_capacity=1 << 14, win_capacity=1 << 14, max_batch=1 << 15,
+                    flags=rl.OPT_PIPELINE if pipeline else 0)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    dev = torch.device("cuda", 0)
+    parts = split(tr, sizes)
+    ins, outs = [], []
+    for key, ts, n, cfg, _ in parts:     # inputs complete before the first call
+        ins.append([torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+                    for x in (key, ts, n, cfg.view(np.int32))])
+        m = key.size
+        outs.append([torch.empty(m, dtype=torch.uint8, device=dev)] +
+                    [torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)] +
+                    [torch.empty(m, dtype=torch.float64, device=dev)])
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for (k, t, n, c), o in zip(ins, outs):
+        eng.decide_device(k.numel(), k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
+                          *[x.data_ptr() for x in o], stream)
+    torch.cuda.synchronize()
+    assert eng.sync() == 0, eng.last_error()
+    for i, ((key, ts, n, cfg, _), o) in enumerate(zip(parts, outs)):
+        ref = sim.decide(key, ts, n, cfg)
+        res = rl.Decisions(*[x.cpu().numpy() for x in o])
+        assert_same(res, ref, configs, cfg, what=f"batch {i}")
