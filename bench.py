@@ -187,6 +187,7 @@ def main():
         "sort_pass": stage_ms[1] / nbat / st.sort_passes,
         "segments": stage_ms[2] / nbat,
         "replay": stage_ms[3] / nbat,
+        "finish": stage_ms[4] / nbat,
     }
     dom = max(per_launch_ms, key=per_launch_ms.get)
     s_alg = max(STATE_BYTES[a] for a in algs)
@@ -216,9 +217,9 @@ def main():
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
                           "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
-                          "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
+                          "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]], "near_setup_x16": int(dbgw[39]) * 16,
                           "hw_id": [hex(int(x)) for x in dbgw[40:45]]},
-        "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay"],
+        "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
                                                     (stage_ms / nbat).tolist())},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -126,11 +126,13 @@ __global__ void k_q14(const double* in, double* out, uint32_t n) {
 
 namespace {
 
-constexpr int NSTAGES = 4;
+constexpr int NSTAGES = 5;
+constexpr int NSETS = 3;          // batch buffer sets: grouping b+1 | replay b | finish b-1
+constexpr int GROUP_LDS = 4096;   // LDS floor of the grouping / finish kernels (see rl_engine::chain_pad)
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
 constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0..3] list counts (heavy TB, light, heavy window, huge TB)
-                                               // [4] chain queue [5] per-thread queue
+                                               // [4] chain queue [5] per-thread queue [6] per-wave queue
 constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iterations [2] max rounds
                                                // [3..6] round ends (full, stop, partial, first window)
                                                // [8..19] timers [20] exact tiles [21] serial steps
@@ -150,11 +152,14 @@ int bitlen(uint64_t v) {
 
 }  // namespace
 
-// Per-batch device buffers.  Two sets: with RL_OPT_PIPELINE, batch b's front
-// half (probe, sort, segments, permute) runs on the engine's front stream
-// while batch b-1's back half (replay, expansion, unpermute) still runs on the
-// caller's stream; set b & 1 is reused by batch b+2 only after batch b's back
-// half (back_done).
+// Per-batch device buffers.  A batch runs in three parts on three engine
+// streams: grouping (probe, sort, segments, permute) on `front`, the replay
+// (k_tb_chain) on `chain`, the finish (run expansion, unpermute) on `tail`.
+// The replays are ordered on `chain` (each one reads the table state the
+// previous one wrote); nothing else orders batches, so batch b+1's grouping
+// and batch b-1's finish overlap batch b's replay.  NSETS buffer sets: set
+// b mod NSETS is reused by batch b+NSETS only after batch b's finish.  The
+// caller's stream waits for the finish of every batch it enqueued.
 struct BatchSet {
     uint32_t *sk0 = nullptr, *sk1 = nullptr, *sv0 = nullptr, *sv1 = nullptr;
     SegRec* list[4] = {nullptr, nullptr, nullptr, nullptr};   // heavy TB, light, heavy window, huge TB
@@ -171,7 +176,7 @@ struct BatchSet {
     uint32_t* zero = nullptr;     // ctrl words + look-back status (memset per batch)
     uint32_t* ctrl = nullptr;
     uint32_t* status = nullptr;
-    hipEvent_t front_done = nullptr, back_done = nullptr;
+    hipEvent_t front_done = nullptr, chain_done = nullptr, back_done = nullptr;
     bool used = false;
 };
 
@@ -179,8 +184,14 @@ struct rl_engine {
     int device = 0;
     int32_t profile = PROFILE_REDIS7;
     uint32_t flags = 0;
-    hipStream_t stream = nullptr;     // the engine's stream (host API; device API without a stream)
-    hipStream_t front = nullptr;      // front halves
+    // the engine's stream (host API, device API without a stream, setup) is
+    // `tail`: with the caller's stream the engine then uses four streams, one
+    // hardware queue each at HIP's default of four queues per process (streams
+    // sharing a queue would serialize the replay and the finish)
+    hipStream_t stream = nullptr;
+    hipStream_t front = nullptr;      // grouping
+    hipStream_t chain = nullptr;      // replays, in batch order
+    hipStream_t tail = nullptr;       // finishes
     hipEvent_t ev_in = nullptr;       // inputs ready (non-pipelined device API, host API)
     std::string err;
 
@@ -197,14 +208,18 @@ struct rl_engine {
 
     uint32_t max_batch = 0;
     uint32_t max_tiles = 0;
-    BatchSet set[2];
-    int next_set = 0, last_set = 0;
+    BatchSet set[NSETS];
+    int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
     size_t zero_bytes = 0;
     int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
     int probe_grid = 1024;      // k_probe blocks at most
     int perm_grid = 1024;       // k_permute / k_unpermute blocks at most
     uint32_t heavy_min = 32;    // segments this long replay cooperatively
     uint32_t huge_min = 4096;   // token-bucket segments this long are dequeued first
+    // dynamic LDS that makes a k_tb_chain block fill its CU's LDS: with two
+    // batches in flight, the other batches' grouping and finish kernels (each launched with
+    // GROUP_LDS bytes at least) then never share a CU with a chain
+    size_t chain_pad[2] = {0, 0};
     uint32_t* d_eflags = nullptr;
 
     // host-API staging (device side)
@@ -216,11 +231,11 @@ struct rl_engine {
     double* d_tok = nullptr;
 
     // timing: front start, after probe, after sort, after segments+permute
-    // (front stream); back start, back end (launch stream)
+    // (front); replay start, end (chain); finish start, end (tail)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::array<hipEvent_t, 6>> ev_pending;
-    double stage_ms[NSTAGES] = {0, 0, 0, 0};
+    std::vector<std::array<hipEvent_t, 8>> ev_pending;
+    double stage_ms[NSTAGES] = {0, 0, 0, 0, 0};
     uint64_t timed_batches = 0;
 
     rl_stats stats{};
@@ -249,6 +264,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.zero);
     if (B.front_done) (void)hipEventDestroy(B.front_done);
     if (B.back_done) (void)hipEventDestroy(B.back_done);
+    if (B.chain_done) (void)hipEventDestroy(B.chain_done);
 }
 
 static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes) {
@@ -283,6 +299,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes) {
     ok &= hipMalloc(&B.zero, zero_bytes) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.front_done, hipEventDisableTiming) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.back_done, hipEventDisableTiming) == hipSuccess;
+    ok &= hipEventCreateWithFlags(&B.chain_done, hipEventDisableTiming) == hipSuccess;
     if (!ok) return false;
     B.ctrl = B.zero;
     B.status = B.zero + CTRL_WORDS;
@@ -301,13 +318,16 @@ static void free_all(rl_engine* e) {
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->ev_in) (void)hipEventDestroy(e->ev_in);
     if (e->front) (void)hipStreamDestroy(e->front);
-    if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->chain) (void)hipStreamDestroy(e->chain);
+    if (e->tail) (void)hipStreamDestroy(e->tail);
 }
 
 // every queued kernel of the engine has finished (the engine's streams and,
 // through the back_done events, any caller stream a batch was enqueued on)
 static int drain(rl_engine* e) {
     HIPCHK(e, hipStreamSynchronize(e->front));
+    HIPCHK(e, hipStreamSynchronize(e->chain));
+    HIPCHK(e, hipStreamSynchronize(e->tail));
     for (auto& B : e->set)
         if (B.used) HIPCHK(e, hipEventSynchronize(B.back_done));
     HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -336,8 +356,10 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
 
     auto bail = [&](int code) { int r = code; free_all(e); delete e; return r; };
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipStreamCreateWithFlags(&e->chain, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipStreamCreateWithFlags(&e->tail, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    e->stream = e->tail;
     if (hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
     size_t M = e->max_batch;
     e->cfg_cap = 64;
@@ -369,6 +391,17 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
     if (const char* v = getenv("RL_PROBE_GRID")) e->probe_grid = atoi(v);
     if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
+    {
+        int dev_lds = 0;
+        (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, e->device);
+        hipFuncAttributes fa[2];
+        if (hipFuncGetAttributes(&fa[0], reinterpret_cast<const void*>(&k_tb_chain<true>)) != hipSuccess ||
+            hipFuncGetAttributes(&fa[1], reinterpret_cast<const void*>(&k_tb_chain<false>)) != hipSuccess)
+            return bail(RL_EDEVICE);
+        for (int k = 0; k < 2; k++)
+            if (dev_lds > (int)fa[k].sharedSizeBytes + GROUP_LDS)
+                e->chain_pad[k] = (size_t)dev_lds - fa[k].sharedSizeBytes - GROUP_LDS + 256;
+    }
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
     *out = e;
@@ -425,21 +458,21 @@ static hipEvent_t take_event(rl_engine* e) {
     return ev;
 }
 
-// enqueue one batch of m <= max_batch requests: front half on e->front, back
-// half on s.  inputs_ready: the caller guarantees the input arrays are
-// complete now (RL_OPT_PIPELINE); otherwise the front half waits for s.
+// enqueue one batch of m <= max_batch requests (see BatchSet); s waits for
+// its finish.  inputs_ready: the caller guarantees the input arrays are
+// complete now (RL_OPT_PIPELINE); otherwise the grouping waits for s.
 static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, bool inputs_ready) {
     if (m == 0) return RL_OK;
     BatchSet& B = e->set[e->next_set];
     e->last_set = e->next_set;
-    e->next_set ^= 1;
+    e->next_set = (e->next_set + 1) % NSETS;
     hipStream_t f = e->front;
     if (!inputs_ready) {
         HIPCHK(e, hipEventRecord(e->ev_in, s));
         HIPCHK(e, hipStreamWaitEvent(f, e->ev_in, 0));
     }
     if (B.used) HIPCHK(e, hipStreamWaitEvent(f, B.back_done, 0));   // set reuse
-    std::array<hipEvent_t, 6> ev{};
+    std::array<hipEvent_t, 8> ev{};
     if (e->timing) {
         for (auto& x : ev) x = take_event(e);
         (void)hipEventRecord(ev[0], f);
@@ -472,7 +505,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
     const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr};
-    k_segments<<<sgrid, 256, 0, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
+    k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
                                       std::max(e->huge_min, e->heavy_min), lists);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, B.p_sms, B.o_dec, B.o_rem, B.o_retry, B.o_reset, B.o_tok};
@@ -480,32 +513,39 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     // the TB reset time is state-independent: k_permute writes it straight
     // into the sorted result buffer
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
-    k_permute<<<pgrid, 256, 0, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, a, ps, pre);
+    k_permute<<<pgrid, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, a, ps, pre);
     if (e->timing) (void)hipEventRecord(ev[3], f);
     HIPCHK(e, hipEventRecord(B.front_done, f));
 
-    // back half: the replay needs this batch's front half and the previous
-    // batch's back half (stream order on s) for the table state
-    HIPCHK(e, hipStreamWaitEvent(s, B.front_done, 0));
-    if (e->timing) (void)hipEventRecord(ev[4], s);
+    // replay: after this batch's grouping and the previous replay (stream
+    // order on `chain`: the table state)
+    hipStream_t c = e->chain, t = e->tail;
+    HIPCHK(e, hipStreamWaitEvent(c, B.front_done, 0));
+    if (e->timing) (void)hipEventRecord(ev[4], c);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
     if (ncfg <= (uint32_t)MAX_LCFG)
-        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
+        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, e->chain_pad[0], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
                                                            e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
                                                            B.runs);
     else
-        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, 0, s>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
+        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, e->chain_pad[1], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
                                                             e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
                                                             B.runs);
-    k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, 0, s>>>(
+    if (e->timing) (void)hipEventRecord(ev[5], c);
+    HIPCHK(e, hipEventRecord(B.chain_done, c));
+    // finish: outputs of the committed runs, results to the caller's order
+    HIPCHK(e, hipStreamWaitEvent(t, B.chain_done, 0));
+    if (e->timing) (void)hipEventRecord(ev[6], t);
+    k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
-    k_unpermute<<<pgrid, 256, 0, s>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
+    k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     if (e->timing) {
-        (void)hipEventRecord(ev[5], s);
+        (void)hipEventRecord(ev[7], t);
         e->ev_pending.push_back(ev);
     }
-    HIPCHK(e, hipEventRecord(B.back_done, s));
+    HIPCHK(e, hipEventRecord(B.back_done, t));
+    HIPCHK(e, hipStreamWaitEvent(s, B.back_done, 0));
     B.used = true;
     HIPCHK(e, hipGetLastError());
     e->stats.batches++;
@@ -625,8 +665,8 @@ extern "C" int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint
     if (!e) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     for (auto& ev : e->ev_pending) {
-        HIPCHK(e, hipEventSynchronize(ev[5]));
-        static const int from[NSTAGES] = {0, 1, 2, 4}, to[NSTAGES] = {1, 2, 3, 5};
+        HIPCHK(e, hipEventSynchronize(ev[7]));
+        static const int from[NSTAGES] = {0, 1, 2, 4, 6}, to[NSTAGES] = {1, 2, 3, 5, 7};
         for (int k = 0; k < NSTAGES; k++) {
             float t = 0;
             HIPCHK(e, hipEventElapsedTime(&t, ev[from[k]], ev[to[k]]));

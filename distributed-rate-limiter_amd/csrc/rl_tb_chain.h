@@ -157,6 +157,11 @@ __device__ inline double wave_reduce_f64(double v, double ident, Op op) {
     v = op(v, dpp_f64<0x143, 0xc>(v, ident));
     return readlane_f64(v, 63);
 }
+__device__ inline int64_t readfirstlane_i64(int64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 __device__ inline uint32_t first_lane(uint64_t m) { return m ? (uint32_t)__ffsll((unsigned long long)m) - 1 : 64u; }
 // arr[i] of a small register array without dynamic indexing (which would
 // place the array in scratch memory)
@@ -335,7 +340,11 @@ __device__ __attribute__((always_inline)) inline uint32_t exact_span(const Src& 
     const int64_t incl = wave_incl_scan_i64(S);
     int64_t st = D0 + incl - S + (lane ? goff : 0);
     const uint32_t last = len ? (len - 1) / K : 0u;
-    for (;;) {
+    for (uint32_t it = 0;; it++) {
+        if (it > 64u) {            // cannot happen (one more exact lane per pass); never hang on it
+            Dend = D0;
+            return 0xffffffffu;
+        }
         double D = (double)st, Db = 0.0;
         uint32_t bq = NO_STOP;
 #pragma unroll
@@ -482,7 +491,8 @@ struct ChOutcome {
 template <int MODE>
 __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShared& sh, const ChState& s, double P,
                                                                      double R, const ReqArgs& a, const TbRuns& runs,
-                                                                     uint32_t& iters, uint32_t* dbg) {
+                                                                     uint32_t* eflags, uint32_t& iters,
+                                                                     uint32_t* dbg) {
     const uint32_t lane = threadIdx.x & 63;
 #ifdef RL_STAMPS
     const uint64_t t_in = __builtin_amdgcn_s_memtime();
@@ -492,27 +502,25 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
     const uint32_t nt = (s.ccnt + CH_TILE - 1) / CH_TILE;
     const double LO = MODE == QM_DEC ? (double)DEC_LO : (double)BIN_LO;
     const double HI = MODE == QM_DEC ? (double)DEC_HI : (double)BIN_HI;
-    // tile prefix sums and near-list prefix (tiles before the first overflow)
-    int64_t TS[CH_NP];
-    uint32_t NPF[CH_NP + 1];
-    uint32_t ovt = nt;
-    {
-        int64_t acc = 0;
-        uint32_t nacc = 0;
+    // one lane per tile: lane t < nt holds tile t; tile prefix sums and the
+    // near-list prefix (tiles before the first overflowing list) by wave scans
+    const bool tv = lane < nt;
+    const uint32_t tl = tv ? lane : 0u;
+    const ChTile T = sh.tile[cb][tl];
+    const uint32_t ovt = min(first_lane(__ballot(tv && T.nc > (uint32_t)CH_NE)), nt);
+    const int64_t Sl = tv ? T.S : 0;
+    const int64_t TS_t = wave_incl_scan_i64(Sl) - Sl;                 // nominal sum before tile t
+    const uint32_t ncl = (tv && lane < ovt) ? T.nc : 0u;
+    const uint32_t np1 = wave_scan_u32(ncl, 0u, [](uint32_t x, uint32_t y) { return x + y; });
+    const uint32_t np0 = np1 - ncl;                                   // near entries before tile t
+    const uint32_t ne = (uint32_t)__builtin_amdgcn_readlane((int)np1, 63);
+    uint32_t NPF[CH_NP];                                              // wave-uniform copies
 #pragma unroll
-        for (int t = 0; t < CH_NP; t++) {
-            TS[t] = acc;
-            NPF[t] = nacc;
-            if ((uint32_t)t < nt) {
-                acc += sh.tile[cb][t].S;
-                const uint32_t nc = sh.tile[cb][t].nc;
-                if (ovt == nt && nc > (uint32_t)CH_NE) ovt = t;
-                if ((uint32_t)t < ovt) nacc += nc;
-            }
-        }
-        NPF[CH_NP] = nacc;
-    }
-    const uint32_t ne = NPF[CH_NP];
+    for (int u = 0; u < CH_NP; u++) NPF[u] = (uint32_t)__builtin_amdgcn_readlane((int)np0, u);
+    const double tbase = (double)(s.D + TS_t);                        // nominal start of tile t
+#ifdef RL_STAMPS
+    if (dbg && lane == 0 && s.hot) atomicAdd(&dbg[39], (uint32_t)((__builtin_amdgcn_s_memtime() - t_in) >> 4));
+#endif
 
     // Near steps in sequence order, 64 at a time.  A step's exact result
     // depends on its exact predecessor = nominal + (offset before it); far
@@ -532,7 +540,7 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
 #pragma unroll
             for (int u = 1; u < CH_NP; u++) t += g >= NPF[u] ? 1u : 0u;
             const uint32_t k = v ? g - pick(NPF, t) : 0u;
-            const double pn = (double)(s.D + pick(TS, t)) + sh.ne_pred[cb][t][k];
+            const double pn = __shfl(tbase, (int)t) + sh.ne_pred[cb][t][k];
             const double ad = sh.ne_add[cb][t][k];
             const double th = sh.ne_th[cb][t][k];
             const double r = rint(ad * P);
@@ -574,15 +582,11 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
 
     // Tile checks, one lane per tile: a tile whose bounds exclude a regime
     // exit is committed as a run; the first other one is replayed exactly.
-    const bool tv = lane < nt;
-    const uint32_t tl = tv ? lane : 0u;
-    const ChTile T = sh.tile[cb][tl];
-    const uint32_t npf0 = pick(NPF, tl), npf1 = pick(NPF, tl + 1);
-    const uint32_t i0 = npf0 < nres ? npf0 : nres, i1 = npf1 < nres ? npf1 : nres;
+    const uint32_t i0 = np0 < nres ? np0 : nres, i1 = np1 < nres ? np1 : nres;
     const int32_t off_in = i0 ? sh.ne_off[i0 - 1] : 0;
     const int32_t off_out = i1 ? sh.ne_off[i1 - 1] : 0;
-    const bool forced = tl >= ovt || (nstop != NO_STOP && nstop < npf1) || T.ev != NO_STOP;
-    const int64_t Dt = s.D + pick(TS, tl) + off_in;
+    const bool forced = tl >= ovt || (nstop != NO_STOP && nstop < np1) || T.ev != NO_STOP;
+    const int64_t Dt = s.D + TS_t + off_in;
     const int64_t D1 = Dt + T.S + (off_out - off_in);
     {
         const double dD = (double)Dt, nc = (double)T.nc;
@@ -612,7 +616,7 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
             const uint32_t cpos = s.cfirst + c * CH_TILE;
             const uint32_t clen = (s.ccnt - c * CH_TILE) < CH_TILE ? (s.ccnt - c * CH_TILE) : CH_TILE;
             const int64_t Dc = readlane_i64(Dt, c);
-            const uint32_t cn0 = pick(NPF, c);
+            const uint32_t cn0 = (uint32_t)__builtin_amdgcn_readlane((int)np0, (int)c);
             const int32_t cin = (int32_t)__builtin_amdgcn_readlane(off_in, (int)c);
             int32_t goff = 0;
             if (c < ovt) {
@@ -621,7 +625,12 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 goff = (gi > cn0 && gc) ? sh.ne_off[gc - 1] - cin : 0;
             }
             int64_t Dq = 0;
-            const uint32_t brk = exact_span<MODE, false>(RingSrc{sh}, cpos, clen, Dc, goff, P, R, Dq, a, iters);
+            uint32_t brk = exact_span<MODE, false>(RingSrc{sh}, cpos, clen, Dc, goff, P, R, Dq, a, iters);
+            if (brk > clen) {       // (never) give up on the window: one exact serial step
+                if (lane == 0) atomicOr(eflags, EF_INTERNAL);
+                brk = 0;
+                Dq = Dc;
+            }
             if (dbg && lane == 0) atomicAdd(&dbg[20], 1u);
             if (lane == 0 && brk) {
                 runs.len[cpos] = (uint16_t)brk;
@@ -649,7 +658,115 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
     }
 }
 
-// Replay one heavy token-bucket segment [j0, j1) with the whole block.
+// Exact serial steps by one wave (every lane computes the same values, lane 0
+// writes): from the exact stored state (D, E) before position q, the step at
+// q when `force` (a step that leaves the regime), then on while the state is
+// off the fast decades or the last step left the regime -- at most
+// CH_SERIAL steps and never at or past lim.  add_at(p): TbPre::add of p.
+struct SerialOut {
+    uint32_t q;        // next position
+    int64_t D;         // exact stored state before it
+    int32_t E;
+    int32_t mode;
+    uint32_t steps;
+};
+
+template <typename AddAt>
+__device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt add_at, uint32_t q, int64_t D, int32_t E,
+                                                                       bool force, uint32_t lim, uint32_t j1,
+                                                                       const CfgDev* __restrict__ cfgs,
+                                                                       int32_t profile, const ReqArgs& a) {
+    const uint32_t lane = threadIdx.x & 63;
+    int32_t mode = fast_mode(D, E, profile);
+    double Ps = 1.0, Rs = 1.0;
+    if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
+    const uint32_t pq = q + lane;                   // n and cfg of the next 64 positions, one load
+    const int64_t nvec = pq < j1 ? a.n[pq] : 1;
+    const uint32_t cvec = pq < j1 ? a.cfg[pq] : 0u;
+    uint32_t k = 0;
+    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
+        const double add = add_at(q);
+        const bool alive = add == add;
+        const int64_t nn = readlane_i64(nvec, k);
+        const CfgDev& C = cfgs[(uint32_t)__builtin_amdgcn_readlane((int)cvec, (int)k)];
+        const TbEval v = tb_eval(mode, D, E, Ps, Rs, alive, alive ? add : 0.0, C.limit_d, (double)nn, profile);
+        if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
+        force = v.allowed || v.clamped || !alive;
+        if (mode != QM_NONE && v.inrange) {
+            D = v.Dact;                     // same decade / binade (sign may flip)
+            mode = fast_mode(D, E, profile);
+        } else {
+            const TbQ nq = tb_quant(v.tokens, profile);
+            D = nq.D;
+            E = nq.E;
+            mode = fast_mode(D, E, profile);
+            if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
+        }
+        q++;
+    }
+    return SerialOut{q, D, E, mode, k};
+}
+
+// TbPre::{add, th} from HBM, with the segment head's add computed at replay
+struct HeadSrc {
+    const double* a;
+    const double* t;
+    uint32_t j0;
+    double add0;
+    __device__ double add(uint32_t p) const { return p == j0 ? add0 : a[p]; }
+    __device__ double th(uint32_t p) const { return t[p]; }
+};
+
+// Replay one heavy (not huge) token-bucket segment [j0, j1) with ONE wave:
+// exact_span over CH_TILE requests at a time, writing every result, and exact
+// serial steps wherever a step leaves the regime.  No producers, no runs:
+// for a few thousand requests this beats a block-wide chain round.
+__device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, uint32_t j0, uint32_t j1,
+                                                                  const CfgDev* __restrict__ cfgs, int32_t profile,
+                                                                  const ReqArgs& a, const TbPre& pre,
+                                                                  uint32_t* eflags, uint32_t& iters) {
+    const TbQ q0 = tb_quant(e->tok, profile);
+    const HeadSrc src{pre.add, pre.th, j0, tb_head_add(e, j0, cfgs, profile, a)};
+    int64_t D = q0.D;
+    int32_t E = q0.E;
+    int32_t mode = fast_mode(D, E, profile);
+    uint32_t pos = j0;
+    for (uint32_t guard = 0; pos < j1; guard++) {
+        if (guard > 2u * (j1 - j0) + 8u) {        // each pass advances pos; never hang on it
+            if ((threadIdx.x & 63) == 0) atomicOr(eflags, EF_INTERNAL | 0x100u);
+            return;
+        }
+        if (mode != QM_NONE) {
+            double P, R;
+            mode_scale(mode, E, P, R);
+            const uint32_t len = (j1 - pos) < CH_TILE ? (j1 - pos) : CH_TILE;
+            int64_t Dq = D;
+            const uint32_t brk = mode == QM_DEC ? exact_span<QM_DEC, true>(src, pos, len, D, 0, P, R, Dq, a, iters)
+                                                : exact_span<QM_BIN, true>(src, pos, len, D, 0, P, R, Dq, a, iters);
+            if (brk > len) {
+                if ((threadIdx.x & 63) == 0) atomicOr(eflags, EF_INTERNAL | 0x200u);
+                return;
+            }
+            D = readfirstlane_i64(Dq);
+            pos += (uint32_t)__builtin_amdgcn_readfirstlane((int)brk);
+            if (brk == len) continue;
+        }
+        const SerialOut so = serial_steps([&](uint32_t p) { return src.add(p); }, pos, D, E, true, j1, j1, cfgs,
+                                          profile, a);
+        // wave-uniform by construction; say so (the loop and its ballots stay uniform)
+        pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)so.q);
+        D = readfirstlane_i64(so.D);
+        E = __builtin_amdgcn_readfirstlane(so.E);
+        mode = __builtin_amdgcn_readfirstlane(so.mode);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        e->tok = tb_value(D, E, profile);
+        e->last = pre.lq[j1 - 1];
+        e->when = pre.when[j1 - 1];
+    }
+}
+
+// Replay one huge token-bucket segment [j0, j1) with the whole block.
 template <bool LCFG>
 __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh, TbEntry* e, uint32_t j0, uint32_t j1,
                                                                 const CfgDev* __restrict__ cfgs, int32_t profile,
@@ -730,8 +847,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             ChOutcome o{CH_PARTIAL, s.pfirst, s.D};
             bool restart = true, force = false;
             if (s.ccnt > 0) {
-                o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, R, a, runs, iters, dbg)
-                                     : ch_resolve<QM_BIN>(sh, s, P, R, a, runs, iters, dbg);
+                o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, R, a, runs, eflags, iters, dbg)
+                                     : ch_resolve<QM_BIN>(sh, s, P, R, a, runs, eflags, iters, dbg);
                 if (dbg && lane == 0) atomicAdd(&dbg[3 + o.kind], 1u);
                 CH_T(t1);
                 cyc[o.kind == CH_FULL ? 0 : 1] += t1 - t0;
@@ -756,47 +873,19 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             } else {
                 // exact serial steps: the exiting step, then on while the state
                 // is off the fast decades or the last step left the regime
-                uint32_t q = o.q;
-                int64_t D = o.D;
-                int32_t E = s.E;
-                int32_t mode = fast_mode(D, E, profile);
-                double Ps = 1.0, Rs = 1.0;
-                if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
                 const uint32_t lim = (j1 - s.pfirst) < CH_W ? j1 : s.pfirst + CH_W;   // resident in the ring
-                const uint32_t pq = q + lane;
-                const int64_t nvec = pq < j1 ? a.n[pq] : 1;
-                const uint32_t cvec = pq < j1 ? a.cfg[pq] : 0u;
-                for (uint32_t k = 0; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
-                    const double add = ring_add(sh, q);
-                    const bool alive = add == add;
-                    const int64_t nn = readlane_i64(nvec, k);
-                    const CfgDev& C = cfgs[(uint32_t)__builtin_amdgcn_readlane((int)cvec, (int)k)];
-                    const TbEval v = tb_eval(mode, D, E, Ps, Rs, alive, alive ? add : 0.0, C.limit_d,
-                                             (double)nn, profile);
-                    if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
-                    force = v.allowed || v.clamped || !alive;
-                    if (mode != QM_NONE && v.inrange) {
-                        D = v.Dact;                     // same decade / binade (sign may flip)
-                        mode = fast_mode(D, E, profile);
-                    } else {
-                        const TbQ nq = tb_quant(v.tokens, profile);
-                        D = nq.D;
-                        E = nq.E;
-                        mode = fast_mode(D, E, profile);
-                        if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
-                    }
-                    q++;
-                    nserial++;
-                }
+                const SerialOut so = serial_steps([&](uint32_t p) { return ring_add(sh, p); }, o.q, o.D, s.E, force,
+                                                  lim, j1, cfgs, profile, a);
+                nserial += so.steps;
                 CH_T(t1);
                 cyc[2] += t1 - t0;
                 t0 = t1;
-                nx.D = D;
-                nx.E = E;
-                nx.mode = mode;
-                nx.cfirst = q;
+                nx.D = so.D;
+                nx.E = so.E;
+                nx.mode = so.mode;
+                nx.cfirst = so.q;
                 nx.ccnt = 0;
-                nx.pfirst = q;
+                nx.pfirst = so.q;
             }
             if (lane == 0) sh.st[par ^ 1u] = nx;
         }
@@ -876,10 +965,11 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
     }
 }
 
-// The replay kernel.  Phase 1: huge then heavy token-bucket segments, one per
-// block (the chain).  Phase 2, as blocks run out of chains (the hot keys'
-// blocks are still busy): heavy window segments, then light segments of any
-// algorithm, one per thread, serial (replay_*_serial).
+// The replay kernel.  Phase 1: huge token-bucket segments, one per block (the
+// chain), longest first.  Phase 2: heavy token-bucket segments, one per wave
+// (wave_segment).  Phase 3: heavy window segments, then light segments of any
+// algorithm, one per thread, serial (replay_*_serial).  The hot keys' blocks
+// stay in phase 1 while the others drain phases 2-3.
 template <bool LCFG>
 __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restrict__ sk, SegLists L, uint32_t* qctr,
                                                        uint32_t win_base, TbEntry* tb, WinEntry* win,
@@ -900,13 +990,25 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         __syncthreads();
         const uint32_t u = s_u;
         __syncthreads();
-        if (u >= nhuge + nheavy) break;
-        const SegRec sg = u < nhuge ? L.list[3][u] : L.list[0][u - nhuge];
+        if (u >= nhuge) break;
+        const SegRec sg = L.list[3][u];
         const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
         ch_segment<LCFG>(sh, &tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
         __syncthreads();
         if (threadIdx.x == 0 && dbg) atomicMax(&dbg[8], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seg));
     }
+    {
+        uint32_t iters = 0;
+        for (;;) {
+            uint32_t u = 0;
+            if ((threadIdx.x & 63) == 0) u = atomicAdd(&qctr[2], 1u);
+            u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+            if (u >= nheavy) break;
+            const SegRec sg = L.list[0][u];
+            wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
+        }
+    }
+    __syncthreads();
     const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)CH_BLOCK);

@@ -222,9 +222,9 @@ class Engine:
         lib.rl_engine_set_timing(self.h, 1 if on else 0)
 
     def stage_times(self):
-        ms = np.zeros(4, np.float64)
+        ms = np.zeros(5, np.float64)
         nb = C.c_uint64()
-        lib.rl_engine_stage_times(self.h, _ptr(ms), 4, C.byref(nb))
+        lib.rl_engine_stage_times(self.h, _ptr(ms), 5, C.byref(nb))
         return ms, nb.value
 
     def q14_device(self, x: np.ndarray) -> np.ndarray:

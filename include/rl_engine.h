@@ -130,7 +130,8 @@ int rl_engine_stats(rl_engine* e, rl_stats* out);
 
 /* per-stage device time (ms) accumulated since the last call, measured with
  * HIP events on the stream the kernels run on; stages: 0 probe, 1 sort,
- * 2 segments, 3 replay.  Requires rl_engine_set_timing(e, 1). */
+ * 2 segments + permute, 3 replay (k_tb_chain), 4 finish (run expansion +
+ * unpermute).  Requires rl_engine_set_timing(e, 1). */
 int rl_engine_set_timing(rl_engine* e, int on);
 int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint64_t* batches);
 /* diagnostic: the last batch's replay debug counters (up to 88 words; layout in rl_engine.hip CTRL_DBG) */
