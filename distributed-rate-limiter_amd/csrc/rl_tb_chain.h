@@ -766,6 +766,158 @@ __device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, u
     }
 }
 
+// Replay one heavy fixed / sliding window segment [j0, j1) with ONE wave.
+// Within a window run (consecutive requests of one window start ws) the
+// reference's state transition is a prefix sum: INCRBY adds n to the current
+// window key, whose TTL is set once at creation; SW's previous-window count is
+// constant and its key's TTL is refreshed by every request
+// (fixedwindow.go:21-27, slidingwindow.go:22-30).  So per run: the first
+// request runs exactly (fw_step / sw_step on the exact state: key lookup,
+// expiry, slot allocation), the rest are computed in parallel from a prefix
+// sum of n and checked request by request against every assumption of that
+// shortcut -- the current key alive, no INCRBY overflow, no TTL reset,
+// the previous key's refresh chain -- and any failed check (or a mixed-config
+// segment, or sub-second windows) replays the segment serially instead.
+__device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry* e, uint32_t j0, uint32_t j1,
+                                                                      const CfgDev* __restrict__ cfgs,
+                                                                      int32_t profile, const ReqArgs& a,
+                                                                      uint32_t* eflags) {
+    constexpr int K = CH_K;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t c0 = a.cfg[j0];
+    const CfgDev& C = cfgs[c0];
+    const bool sw = C.alg == ALG_SLIDING_WINDOW;
+    WinState w;
+    w.s[0] = e->s[0];
+    w.s[1] = e->s[1];
+    uint32_t ef = 0;
+    bool ok = C.ttl_c > 0;
+    uint32_t pos = j0;
+    while (ok && pos < j1) {
+        // first request of the run: exact
+        const Req r0 = load_req(a, pos);
+        if (r0.c != c0) { ok = false; break; }
+        const Out o0 = sw ? sw_step(w, r0.t, r0.n, r0.sms, C, profile, ef)
+                          : fw_step(w, r0.t, r0.n, r0.sms, C, profile, ef);
+        if (lane == 0) write_out(a, pos, o0);
+        const int64_t ws = window_start(r0.t, C), pws = ws - C.ttl_c;
+        int ck = -1, pk = -1;
+        for (int k = 0; k < 2; k++) {
+            if (w.s[k].when == ABSENT) continue;
+            if (w.s[k].ws == ws) ck = k;
+            else if (sw && w.s[k].ws == pws) pk = k;
+        }
+        if (o0.decision == DEC_ERROR || ck < 0) { ok = false; break; }
+        const int64_t when_c = w.s[ck].when;
+        const int64_t cnt_p = pk >= 0 ? w.s[pk].cnt : 0;
+        int64_t c_run = w.s[ck].cnt, sms_prev = r0.sms;
+        bool p_alive = pk >= 0;
+        pos++;
+        bool run_end = false;
+        while (ok && !run_end && pos < j1) {
+            // K requests per lane; the run ends at the first other window / config
+            const uint32_t off = lane * K;
+            int64_t t[K], n[K], sm[K];
+            bool same[K];
+            uint32_t firstx = NO_STOP;
+#pragma unroll
+            for (int q = 0; q < K; q++) {
+                const uint32_t j = pos + off + q;
+                const bool v = j < j1;
+                t[q] = v ? a.ts[j] : 0;
+                n[q] = v ? a.n[j] : 0;
+                sm[q] = v ? a.sms[j] : 0;
+                same[q] = v && a.cfg[j] == c0 && window_start(t[q], C) == ws;
+                if (v && !same[q] && firstx == NO_STOP) firstx = off + q;
+            }
+            const uint32_t cend = wave_min_u32(firstx);            // run end in this chunk (relative)
+            const uint32_t lim = min(min(cend, j1 - pos), (uint32_t)(64 * K));
+            run_end = cend != NO_STOP;
+            // prefix sum of n (int64) inside the run, per-request checks
+            int64_t ls = 0;
+#pragma unroll
+            for (int q = 0; q < K; q++)
+                if (off + q < lim) ls += n[q];
+            const int64_t li = wave_incl_scan_i64(ls);
+            int64_t c = c_run + li - ls;                            // count before my first request
+            int64_t sp = __shfl_up(sm[K - 1], 1);                   // server clock of my predecessor
+            if (lane == 0) sp = sms_prev;
+            bool bad = false, pdead = false;
+            uint32_t pdead_at = NO_STOP;
+#pragma unroll
+            for (int q = 0; q < K; q++) {
+                if (off + q >= lim) continue;
+                bad |= incr_overflows(c, n[q]);
+                const int64_t cur = c + n[q];
+                bad |= (double)cur == (double)n[q];                 // would (re)set the TTL
+                bad |= !key_alive(when_c, sm[q], profile);          // current key expired mid-run
+                if (sw && !pdead && !key_alive(expire_when(C.ttl_p, sp), sm[q], profile)) {
+                    pdead = true;
+                    pdead_at = off + q;
+                }
+                sp = sm[q];
+                c = cur;
+            }
+            if (__ballot(bad)) { ok = false; break; }
+            const uint32_t pd = wave_min_u32(pdead_at);             // first request that finds prev dead
+            // outputs
+            c = c_run + li - ls;
+#pragma unroll
+            for (int q = 0; q < K; q++) {
+                if (off + q >= lim) continue;
+                const int64_t cur = c + n[q];
+                c = cur;
+                Out o;
+                o.tokens = 0.0;
+                o.reset_at = wadd(wmul(ws, NS_PER_S), C.window);
+                int64_t count;
+                bool allowed;
+                if (sw) {
+                    const int64_t p = (p_alive && off + q < pd) ? go_f2i((double)cnt_p) : 0;
+                    const int64_t cc = go_f2i((double)cur);
+                    const int64_t elapsed = wsub(t[q], wmul(ws, NS_PER_S));
+                    const double progress = (double)elapsed / (double)C.window;
+                    double weighted = (double)p * (1.0 - progress);
+                    weighted = weighted + (double)cc;
+                    allowed = weighted <= C.limit_d;
+                    count = go_f2i(weighted);
+                } else {
+                    count = go_f2i((double)cur);
+                    allowed = count <= C.limit;
+                }
+                const int64_t rem = wsub(C.limit, count);
+                o.remaining = rem < 0 ? 0 : rem;
+                o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
+                o.retry = allowed ? 0 : until_reset(o.reset_at, t[q]);
+                write_out(a, pos + off + q, o);
+            }
+            // carry to the next chunk
+            const uint32_t lastl = (lim - 1) / K, lastq = (lim - 1) % K;
+            int64_t smv = sm[0];
+#pragma unroll
+            for (int q = 1; q < K; q++) smv = (uint32_t)q == lastq ? sm[q] : smv;
+            sms_prev = readlane_i64(smv, lastl);
+            c_run = readlane_i64(c, lastl);
+            if (pd != NO_STOP) p_alive = false;
+            pos += lim;
+        }
+        if (!ok) break;
+        // the state after the run
+        w.s[ck].cnt = c_run;
+        if (pk >= 0) w.s[pk].when = p_alive ? expire_when(C.ttl_p, sms_prev) : ABSENT;
+    }
+    if (!ok) {
+        // replay the whole segment serially (outputs written so far are rewritten)
+        if (lane == 0) replay_win_serial(e, j0, j1, cfgs, profile, a, eflags);
+        return;
+    }
+    if (lane == 0) {
+        e->s[0] = w.s[0];
+        e->s[1] = w.s[1];
+        if (ef) atomicOr(eflags, ef);
+    }
+}
+
 // Replay one huge token-bucket segment [j0, j1) with the whole block.
 template <bool LCFG>
 __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh, TbEntry* e, uint32_t j0, uint32_t j1,
@@ -966,10 +1118,10 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
 }
 
 // The replay kernel.  Phase 1: huge token-bucket segments, one per block (the
-// chain), longest first.  Phase 2: heavy token-bucket segments, one per wave
-// (wave_segment).  Phase 3: heavy window segments, then light segments of any
-// algorithm, one per thread, serial (replay_*_serial).  The hot keys' blocks
-// stay in phase 1 while the others drain phases 2-3.
+// chain), longest first.  Phase 2: heavy token-bucket segments (wave_segment)
+// and heavy window segments (wave_win_segment), one per wave.  Phase 3: light
+// segments of any algorithm, one per thread, serial (replay_*_serial).  The
+// hot keys' blocks stay in phase 1 while the others drain phases 2-3.
 template <bool LCFG>
 __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restrict__ sk, SegLists L, uint32_t* qctr,
                                                        uint32_t win_base, TbEntry* tb, WinEntry* win,
@@ -1003,9 +1155,14 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
             uint32_t u = 0;
             if ((threadIdx.x & 63) == 0) u = atomicAdd(&qctr[2], 1u);
             u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
-            if (u >= nheavy) break;
-            const SegRec sg = L.list[0][u];
-            wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
+            if (u >= nheavy + nwin) break;
+            if (u < nheavy) {
+                const SegRec sg = L.list[0][u];
+                wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
+            } else {
+                const SegRec sg = L.list[2][u - nheavy];
+                wave_win_segment(&win[sk[sg.j0] - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+            }
         }
     }
     __syncthreads();
@@ -1015,10 +1172,10 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         __syncthreads();
         const uint32_t u0 = s_u;
         __syncthreads();
-        if (u0 >= nwin + nlight) break;
+        if (u0 >= nlight) break;
         const uint32_t u = u0 + threadIdx.x;
-        if (u < nwin + nlight) {
-            const SegRec sg = u < nwin ? L.list[2][u] : L.list[1][u - nwin];
+        if (u < nlight) {
+            const SegRec sg = L.list[1][u];
             const uint32_t k0 = sk[sg.j0];
             if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre);
             else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
