@@ -140,7 +140,9 @@ def main():
     out_retry = torch.empty(m, dtype=torch.int64, device=dev)
     out_reset = torch.empty(m, dtype=torch.int64, device=dev)
     out_tok = torch.empty(m, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # a stream of our own, not the legacy default stream (which would order the
+    # engine's streams behind each call)
+    stream = torch.cuda.Stream(dev).cuda_stream
 
     def step(b):
         k, t, n, c = dev_batches[b]
@@ -190,6 +192,17 @@ def main():
         "finish": stage_ms[4] / nbat,
     }
     dom = max(per_launch_ms, key=per_launch_ms.get)
+    # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
+    # passes (scripts/profile.sh: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)
+    traffic = None
+    kname = {"replay": "k_tb_chain<true>", "probe": "k_probe", "sort_pass": "k_sort_pass<false>",
+             "segments": "k_permute", "finish": "k_unpermute"}[dom]
+    try:
+        tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+        if args.workload == "tb_zipf" and kname in tj["kernels"]:
+            traffic = tj["kernels"][kname]["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        pass
     s_alg = max(STATE_BYTES[a] for a in algs)
     bytes_per_dec = 24 + 32 + 2 * s_alg * (uniq / m)
     achieved = bytes_per_dec * m / (per_launch_ms[dom] / 1e3) / 1e9
@@ -209,14 +222,20 @@ def main():
         "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
                    "profile": "redis7 (Lua %.14g state round trip)", "parallelism": f"key-shard x{world}",
                    "batches_in_flight": 1 if args.no_pipeline else 2},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "bytes_per_decision": bytes_per_dec},
+        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "algorithmic_bytes_per_launch": bytes_per_dec * m,
+                     "bytes_per_decision": bytes_per_dec, "launch_ms": per_launch_ms[dom]},
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
                           "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
+                          "replay_timeline_us": {"hot_start": ((int(dbgw[16]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
+                                                 "hot_end": ((int(dbgw[17]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
+                                                 "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
+                                                 "stamp_before": ((int(dbgw[18]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100 - (1 << 32) / 100 if dbgw[18] else None,
+                                                 "stamp_after": ((int(dbgw[19]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100 if dbgw[19] else None},
                           "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]], "near_setup_x16": int(dbgw[39]) * 16,
                           "hw_id": [hex(int(x)) for x in dbgw[40:45]]},
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],

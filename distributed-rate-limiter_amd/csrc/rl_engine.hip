@@ -115,6 +115,9 @@ __global__ void k_reset(uint64_t key, int64_t ts, const CfgDev* cfgs, uint32_t c
     }
 }
 
+// diagnostic timestamp (10 ns ticks) into *w
+__global__ void k_stamp(uint32_t* w) { *w = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
+
 __global__ void k_q14(const double* in, double* out, uint32_t n) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = rlq::q14(in[i]);
@@ -173,9 +176,10 @@ struct BatchSet {
     double *q_add = nullptr, *q_th = nullptr, *q_lq = nullptr;
     int64_t* q_when = nullptr;
     TbRuns runs{};                // the chain's committed runs (by start position)
-    uint32_t* zero = nullptr;     // ctrl words + look-back status (memset per batch)
+    uint32_t* zero = nullptr;     // ctrl words + look-back status + huge claims (memset per batch)
     uint32_t* ctrl = nullptr;
     uint32_t* status = nullptr;
+    uint32_t* claim = nullptr;
     hipEvent_t front_done = nullptr, chain_done = nullptr, back_done = nullptr;
     bool used = false;
 };
@@ -233,6 +237,7 @@ struct rl_engine {
     // timing: front start, after probe, after sort, after segments+permute
     // (front); replay start, end (chain); finish start, end (tail)
     bool timing = false;
+    bool stamps = false;        // RL_STAMP_KERNELS: timestamps around each replay (debug words 18, 19)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::array<hipEvent_t, 8>> ev_pending;
     double stage_ms[NSTAGES] = {0, 0, 0, 0, 0};
@@ -267,7 +272,7 @@ static void free_set(BatchSet& B) {
     if (B.chain_done) (void)hipEventDestroy(B.chain_done);
 }
 
-static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes) {
+static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_words) {
     bool ok = true;
     ok &= hipMalloc(&B.sk0, 4 * M) == hipSuccess;
     ok &= hipMalloc(&B.sk1, 4 * M) == hipSuccess;
@@ -303,6 +308,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes) {
     if (!ok) return false;
     B.ctrl = B.zero;
     B.status = B.zero + CTRL_WORDS;
+    B.claim = B.status + status_words;
     // run lengths start at 0; k_tb_expand clears every one it consumes
     return hipMemset(B.runs.len, 0, 2 * M) == hipSuccess;
 }
@@ -356,19 +362,38 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
 
     auto bail = [&](int code) { int r = code; free_all(e); delete e; return r; };
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
-    if (hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
-    if (hipStreamCreateWithFlags(&e->chain, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
-    if (hipStreamCreateWithFlags(&e->tail, hipStreamNonBlocking) != hipSuccess) return bail(RL_EDEVICE);
+    {
+        // grouping and finish kernels never use RESERVED_CUS CUs (one per 32):
+        // when a replay is launched those are free, so its first blocks -- the
+        // longest segments -- start at once instead of waiting for a CU that
+        // the other two streams' blocks have left empty
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, e->device) != hipSuccess) return bail(RL_EDEVICE);
+        const int ncu = prop.multiProcessorCount;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int c = 0; c < ncu; c++)
+            if (c % 32 != 31 || ncu < 64) mask[c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(&e->front, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
+            hipExtStreamCreateWithCUMask(&e->tail, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+            return bail(RL_EDEVICE);
+    }
+    {
+        // the replay is the critical path: its blocks are dispatched first
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (hipStreamCreateWithPriority(&e->chain, hipStreamNonBlocking, hi) != hipSuccess) return bail(RL_EDEVICE);
+    }
     e->stream = e->tail;
     if (hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
     size_t M = e->max_batch;
     e->cfg_cap = 64;
-    e->zero_bytes = 4 * (CTRL_WORDS + (size_t)4 * e->max_tiles * RADIX);
+    const size_t status_words = (size_t)4 * e->max_tiles * RADIX;
+    e->zero_bytes = 4 * (CTRL_WORDS + status_words + M / 4096 + 1);
     bool ok = true;
     ok &= hipMalloc(&e->d_cfg, sizeof(CfgDev) * e->cfg_cap) == hipSuccess;
     ok &= hipMalloc(&e->d_tb, sizeof(TbEntry) * e->tb_cap) == hipSuccess;
     ok &= hipMalloc(&e->d_win, sizeof(WinEntry) * e->win_cap) == hipSuccess;
-    for (auto& B : e->set) ok = ok && alloc_set(B, M, e->zero_bytes);
+    for (auto& B : e->set) ok = ok && alloc_set(B, M, e->zero_bytes, status_words);
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
     ok &= hipMalloc(&e->d_key, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_ts, 8 * M) == hipSuccess;
@@ -391,6 +416,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
     if (const char* v = getenv("RL_PROBE_GRID")) e->probe_grid = atoi(v);
     if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
+    e->stamps = getenv("RL_STAMP_KERNELS") != nullptr;
     {
         int dev_lds = 0;
         (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, e->device);
@@ -504,7 +530,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     // sorted keys/values are now in kin/vin
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
-    const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr};
+    const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
     k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
                                       std::max(e->huge_min, e->heavy_min), lists);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
@@ -522,6 +548,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     hipStream_t c = e->chain, t = e->tail;
     HIPCHK(e, hipStreamWaitEvent(c, B.front_done, 0));
     if (e->timing) (void)hipEventRecord(ev[4], c);
+    if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 18);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
     if (ncfg <= (uint32_t)MAX_LCFG)
@@ -532,6 +559,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
         k_tb_chain<false><<<e->coop_grid, CH_BLOCK, e->chain_pad[1], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
                                                             e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
                                                             B.runs);
+    if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 19);
     if (e->timing) (void)hipEventRecord(ev[5], c);
     HIPCHK(e, hipEventRecord(B.chain_done, c));
     // finish: outputs of the committed runs, results to the caller's order

@@ -332,6 +332,7 @@ struct SegRec {
 struct SegLists {
     SegRec* list[4];
     uint32_t* count;      // 4 counters
+    uint32_t* claim;      // per huge segment: claimed by a replay block (zeroed per batch)
 };
 
 }  // namespace rl

@@ -1137,17 +1137,45 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
     }
     const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
     const uint32_t nheavy = L.count[0], nlight = L.count[1], nwin = L.count[2], nhuge = L.count[3];
+    // timeline (10 ns ticks, low 32 bits): dbg[13] = ~first block start,
+    // dbg[14] = last block end, dbg[16/17] = longest segment start / end
+    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
     for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u);
+        // claim the longest unclaimed huge segment (their list is short:
+        // batch / 4096 at most), so the hottest key starts with the first block
+        if (threadIdx.x == 0) {
+            uint32_t got = NO_STOP;
+            if (atomicAdd(&qctr[0], 1u) < nhuge) {
+                for (;;) {
+                    uint32_t best = NO_STOP, blen = 0;
+                    for (uint32_t k = 0; k < nhuge; k++) {
+                        const SegRec r = L.list[3][k];
+                        if (r.len > blen && __hip_atomic_load(&L.claim[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                            best = k;
+                            blen = r.len;
+                        }
+                    }
+                    if (best == NO_STOP) break;
+                    if (atomicCAS(&L.claim[best], 0u, 1u) == 0u) { got = best; break; }
+                }
+            }
+            s_u = got;
+        }
         __syncthreads();
         const uint32_t u = s_u;
         __syncthreads();
-        if (u >= nhuge) break;
+        if (u == NO_STOP) break;
         const SegRec sg = L.list[3][u];
         const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
         ch_segment<LCFG>(sh, &tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
         __syncthreads();
-        if (threadIdx.x == 0 && dbg) atomicMax(&dbg[8], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_seg));
+        if (threadIdx.x == 0 && dbg) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            if (atomicMax(&dbg[8], (uint32_t)(t_end - t_seg)) < (uint32_t)(t_end - t_seg)) {
+                dbg[16] = (uint32_t)t_seg;
+                dbg[17] = (uint32_t)t_end;
+            }
+        }
     }
     {
         uint32_t iters = 0;
@@ -1181,7 +1209,10 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
             else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
     }
-    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
+    if (threadIdx.x == 0 && dbg) {
+        atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
+        atomicMax(&dbg[14], (uint32_t)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 }  // namespace rl

@@ -10,6 +10,7 @@ random accesses of the table probes, whose width is uncalibrated).
 """
 import collections
 import csv
+import json
 import os
 import shutil
 import sys
@@ -49,5 +50,18 @@ for r in stats:
     lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} | "
                  f"{'' if fa is None else f'{fa:.0f}'} | {'' if fa is None else f'{2 * fa * 1024 / 1e6:.2f}'} | "
                  f"{'' if wa is None else f'{wa * 1024 / 1e6:.2f}'} |")
+lines += ["", "2xFETCH: gfx950 FETCH_SIZE counts half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM);",
+          "it is an upper bound for the narrow, random reads (table probes, gathers), whose width is uncalibrated.",
+          "Infinity-Cache hits are counted as fetches (not excluded)."]
 open(os.path.join(dst, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines))
+# per-launch corrected HBM bytes per kernel, read by bench.py (roofline.traffic)
+traffic = {}
+for r in stats:
+    k = short(r["Name"])
+    f, w = pmc.get((k, "FETCH_SIZE")), pmc.get((k, "WRITE_SIZE"))
+    if f and w:
+        traffic[k] = {"bytes_per_launch": 2 * sum(f) / len(f) * 1024 + sum(w) / len(w) * 1024,
+                      "fetch_x2_bytes": 2 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024,
+                      "avg_ns": float(r["AverageNs"])}
+json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
