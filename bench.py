@@ -81,6 +81,10 @@ def cpu_baseline(workload, batch, sample):
 
 
 def main():
+    # one JSON line on stdout: anything native libraries print (the RCCL banner,
+    # ROCm notices) goes to stderr; the line is written to the saved stdout
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -90,6 +94,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
+    ap.add_argument("--route", action="store_true",
+                    help="routed ingress: every rank draws keys from the whole key space and an RCCL "
+                         "all-to-all moves each request to its owner GPU and the result back")
     args = ap.parse_args()
 
     import torch
@@ -100,16 +107,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl")  # RCCL over xGMI: barrier + max-over-ranks only
+    if world > 1 or args.route:
+        # RCCL over xGMI: barrier + max-over-ranks (sharded), plus the request /
+        # result all-to-alls (routed)
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
     gen = make_workload(args.workload, args.batch, rank)
     nb = args.warmup + args.steps
     host = [gen.next_batch() for _ in range(nb)]
-    # this rank's shard of the key space: ids tagged with the owner rank
-    tag = np.uint64(rank) << np.uint64(48)
+    # sharded ingress: this rank's shard of the key space (ids tagged with the
+    # owner rank); routed ingress: the shared key space, routed per batch
+    tag = np.uint64(0 if args.route else rank) << np.uint64(48)
     uniq = np.unique(host[-1][0]).size
     dev_batches = []
     for key, ts, n, cfg in host:
@@ -128,10 +141,11 @@ def main():
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7,
                         tb_capacity=keyspace if need_tb else 1024,
                         win_capacity=keyspace if algs - {1} else 1024,
-                        max_batch=args.batch, device=local_rank,
+                        max_batch=args.batch * (2 if args.route else 1), device=local_rank,
                         # inputs are resident before the timed region: batch b+1's
                         # hash/sort/permute overlaps batch b's replay
-                        flags=0 if args.no_pipeline else rl_amd.OPT_PIPELINE)
+                        # (routed: the inputs come out of the all-to-all on torch's stream)
+                        flags=0 if args.no_pipeline or args.route else rl_amd.OPT_PIPELINE)
     for a, L, W in gen.configs:
         eng.register(a, L, W)
     m = args.batch
@@ -146,9 +160,22 @@ def main():
 
     def step(b):
         k, t, n, c = dev_batches[b]
+        if args.route:
+            import shard
+            shard.route_and_decide_torch(k, t, n, c, decide_owned)
+            return
         eng.decide_device(m, k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
                           out_dec.data_ptr(), out_rem.data_ptr(), out_retry.data_ptr(), out_reset.data_ptr(),
                           out_tok.data_ptr(), stream)
+
+    def decide_owned(k, t, n, c):
+        # the owner's merged requests, on this GPU, enqueued on torch's stream
+        mm = k.numel()
+        o = [torch.empty(mm, dtype=torch.uint8, device=dev)] + \
+            [torch.empty(mm, dtype=torch.int64, device=dev) for _ in range(3)]
+        eng.decide_device(mm, k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
+                          *[x.data_ptr() for x in o], 0, torch.cuda.current_stream(dev).cuda_stream)
+        return o
 
     for b in range(args.warmup):
         step(b)
@@ -220,8 +247,8 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
         "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
-                   "profile": "redis7 (Lua %.14g state round trip)", "parallelism": f"key-shard x{world}",
-                   "batches_in_flight": 1 if args.no_pipeline else 2},
+                   "profile": "redis7 (Lua %.14g state round trip)", "parallelism": (f"routed all-to-all x{world}" if args.route else f"key-shard x{world}"),
+                   "batches_in_flight": 1 if args.no_pipeline or args.route else 2},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": bytes_per_dec * m,
@@ -244,9 +271,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload, m, args.cpu_sample)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
     eng.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

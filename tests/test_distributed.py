@@ -53,11 +53,23 @@ def _worker(rank, world, port, q):
         ref = oracle.OracleSim(0)
         for a, L, W in CONFIGS:
             ref.add_config(a, L, W)
+        import torch
+
+        def decide_t(key, ts, n, cfg):
+            d, r, rt, rs, _ = sim.decide(key.numpy().view(np.uint64), ts.numpy(), n.numpy(),
+                                         cfg.numpy().view(np.uint32))
+            return (torch.from_numpy(d), torch.from_numpy(r), torch.from_numpy(rt), torch.from_numpy(rs))
+
         all_batches = [rank_batches(r) for r in range(world)]
         ok = True
         for b in range(3):
             key, ts, n, cfg = all_batches[rank][b]
-            got = shard.route_and_decide(key, ts, n, cfg, decide)
+            if b % 2 == 0:   # the host (numpy) router
+                got = shard.route_and_decide(key, ts, n, cfg, decide)
+            else:            # the device router (tensors; CPU tensors under gloo here)
+                got = [x.numpy() for x in shard.route_and_decide_torch(
+                    torch.from_numpy(key.view(np.int64)), torch.from_numpy(ts), torch.from_numpy(n),
+                    torch.from_numpy(cfg.view(np.int32)), decide_t)]
             # expectation: one shared limiter over the union, ordered (ts, rank, pos)
             parts = [all_batches[r][b] for r in range(world)]
             U = [np.concatenate([p[f] for p in parts]) for f in range(4)]
@@ -96,6 +108,17 @@ def test_routed_sharding_matches_single_shared_limiter():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_owner_torch_matches_numpy():
+    import torch
+
+    import shard
+    key = np.random.default_rng(9).integers(0, 1 << 63, 100_000).astype(np.uint64) * np.uint64(2) + np.uint64(1)
+    for world in (2, 3, 8):
+        a = shard.owner_of(key, world)
+        b = shard.owner_of_torch(torch.from_numpy(key.view(np.int64)), world).numpy()
+        assert np.array_equal(a, b)
 
 
 def test_owner_partition_is_balanced():
