@@ -66,9 +66,13 @@ typedef struct rl_opts {
 
 /* rl_opts.flags: the device-API input arrays of every rl_decide_batch_device
  * call are complete when the call is made (not produced by work still queued
- * on `stream`).  The engine then overlaps a batch's grouping (hash, sort,
- * permute) with the previous batch's replay, on a second internal stream;
- * results are identical. */
+ * on `stream`).  The engine then runs each batch in three parts on three
+ * internal streams -- grouping (hash, sort, permute), replay, finish -- so
+ * that batch b+1's grouping and batch b-1's finish overlap batch b's replay
+ * (three batches in flight, three internal buffer sets).  Replays stay in
+ * call order; results are identical.  `stream` still orders the results:
+ * work queued on it after the call sees them.  The inputs must stay
+ * unmodified until then. */
 #define RL_OPT_PIPELINE 1u
 
 typedef struct rl_stats {
