@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
+    ap.add_argument("--lat-batches", type=int, default=32,
+                    help="batches of the latency phase (after the timed region): closed loop with the "
+                         "pipeline's depth in flight, per-batch issue->results-complete time")
     ap.add_argument("--route", action="store_true",
                     help="routed ingress: every rank draws keys from the whole key space and an RCCL "
                          "all-to-all moves each request to its owner GPU and the result back")
@@ -119,7 +122,8 @@ def main():
 
     gen = make_workload(args.workload, args.batch, rank)
     nb = args.warmup + args.steps
-    host = [gen.next_batch() for _ in range(nb)]
+    lat_n = 0 if args.route else max(0, args.lat_batches)
+    host = [gen.next_batch() for _ in range(nb + lat_n)]
     # sharded ingress: this rank's shard of the key space (ids tagged with the
     # owner rank); routed ingress: the shared key space, routed per batch
     tag = np.uint64(0 if args.route else rank) << np.uint64(48)
@@ -156,7 +160,8 @@ def main():
     out_tok = torch.empty(m, dtype=torch.float64, device=dev)
     # a stream of our own, not the legacy default stream (which would order the
     # engine's streams behind each call)
-    stream = torch.cuda.Stream(dev).cuda_stream
+    stream_obj = torch.cuda.Stream(dev)
+    stream = stream_obj.cuda_stream
 
     def step(b):
         k, t, n, c = dev_batches[b]
@@ -203,6 +208,31 @@ def main():
     stage_ms, nbat = eng.stage_times()
     st = eng.stats()
     dbgw = eng.debug_words()
+    eng.set_timing(False)
+
+    # latency phase (p99 batch latency of the metric): the next lat_n batches of
+    # the same trace, closed loop with `depth` batches in flight; a batch's
+    # latency runs from the host call to the host seeing its results complete
+    # on the caller's stream (an upper bound: batches are waited for in order)
+    depth = 1 if args.no_pipeline else 3
+    lat = []
+    pend = []
+    for b in range(nb, nb + lat_n):
+        if len(pend) >= depth:
+            tb, ev = pend.pop(0)
+            ev.synchronize()
+            lat.append(time.perf_counter() - tb)
+        tb = time.perf_counter()
+        step(b)
+        ev = torch.cuda.Event()
+        ev.record(stream_obj)
+        pend.append((tb, ev))
+    for tb, ev in pend:
+        ev.synchronize()
+        lat.append(time.perf_counter() - tb)
+    rc = eng.sync()
+    if rc != 0:
+        raise SystemExit(f"engine error during latency phase: {rc} {eng.last_error()}")
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -233,8 +263,14 @@ def main():
     s_alg = max(STATE_BYTES[a] for a in algs)
     bytes_per_dec = 24 + 32 + 2 * s_alg * (uniq / m)
     achieved = bytes_per_dec * m / (per_launch_ms[dom] / 1e3) / 1e9
+    latency = None
+    if lat:
+        la = np.array(lat) * 1e3
+        latency = {"p50_batch_ms": float(np.percentile(la, 50)), "p99_batch_ms": float(np.percentile(la, 99)),
+                   "max_batch_ms": float(la.max()), "batches": int(la.size), "in_flight": depth,
+                   "batch": m, "how": "closed loop after the timed region; host call -> results complete"}
     out = {
-        "metric": "decisions/sec",
+        "metric": "decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency",
         "value": value,
         "unit": "decisions/s",
         "n_gpus": world,
@@ -248,7 +284,7 @@ def main():
         "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
         "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
                    "profile": "redis7 (Lua %.14g state round trip)", "parallelism": (f"routed all-to-all x{world}" if args.route else f"key-shard x{world}"),
-                   "batches_in_flight": 1 if args.no_pipeline or args.route else 2},
+                   "batches_in_flight": 1 if args.no_pipeline or args.route else 3},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": bytes_per_dec * m,
@@ -265,6 +301,7 @@ def main():
                                                  "stamp_after": ((int(dbgw[19]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100 if dbgw[19] else None},
                           "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]], "near_setup_x16": int(dbgw[39]) * 16,
                           "hw_id": [hex(int(x)) for x in dbgw[40:45]]},
+        "latency": latency,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
                                                     (stage_ms / nbat).tolist())},
     }

@@ -61,7 +61,8 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     uint32_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ n,
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
     uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
-    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, ReqArgs a, uint32_t* eflags) {
+    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, ReqArgs a, ReqRec* __restrict__ rec,
+    uint32_t* eflags) {
     __shared__ uint32_t lh[4][RADIX];
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
@@ -84,6 +85,16 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             }
         }
         sk[i] = slot;
+        // one 32-B record per request: k_permute's sorted-order gather then
+        // touches one line fragment instead of four arrays
+        const int64_t t = a.ts[i];
+        ReqRec r;
+        r.ts = t;
+        r.n = nn;
+        r.sms = a.sms ? a.sms[i] : floor_div(t, 1000000LL);
+        r.cfg = c;
+        r.pad = 0;
+        rec[i] = r;
         for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
     }
     if (ef) atomicOr(eflags, ef);
@@ -169,6 +180,7 @@ struct BatchSet {
     // requests and results in sorted order (k_permute / k_unpermute)
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
+    ReqRec* rec = nullptr;        // requests packed in arrival order (k_probe -> k_permute)
     uint8_t* o_dec = nullptr;
     int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
     double* o_tok = nullptr;
@@ -262,6 +274,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.sk0); (void)hipFree(B.sk1); (void)hipFree(B.sv0); (void)hipFree(B.sv1);
     for (auto* l : B.list) (void)hipFree(l);
     (void)hipFree(B.p_ts); (void)hipFree(B.p_n); (void)hipFree(B.p_sms); (void)hipFree(B.p_cfg);
+    (void)hipFree(B.rec);
     (void)hipFree(B.o_dec); (void)hipFree(B.o_rem); (void)hipFree(B.o_retry); (void)hipFree(B.o_reset);
     (void)hipFree(B.o_tok);
     (void)hipFree(B.q_add); (void)hipFree(B.q_th); (void)hipFree(B.q_lq); (void)hipFree(B.q_when);
@@ -286,6 +299,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_n, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.rec, sizeof(ReqRec) * M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
     ok &= hipMalloc(&B.o_rem, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.o_retry, 8 * M) == hipSuccess;
@@ -511,7 +525,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     k_probe<<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
                                                 e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
                                                 e->win_base, e->invalid_key, B.sk0, ghist,
-                                                e->sort_passes, a, e->d_eflags);
+                                                e->sort_passes, a, B.rec, e->d_eflags);
     if (e->timing) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
@@ -539,7 +553,7 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     // the TB reset time is state-independent: k_permute writes it straight
     // into the sorted result buffer
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
-    k_permute<<<pgrid, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, a, ps, pre);
+    k_permute<<<pgrid, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, B.rec, ps, pre);
     if (e->timing) (void)hipEventRecord(ev[3], f);
     HIPCHK(e, hipEventRecord(B.front_done, f));
 
@@ -672,7 +686,12 @@ extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     const uint32_t* ctrl = e->set[e->last_set].ctrl;
     HIPCHK(e, hipMemcpy(c, ctrl + CTRL_NSEG, sizeof c, hipMemcpyDeviceToHost));
     HIPCHK(e, hipMemcpy(d, ctrl + CTRL_DBG, sizeof d, hipMemcpyDeviceToHost));
-    for (int k = 0; k < 6; k++) e->stats.stamp_cycles[k] = ((uint64_t)d[8 + 2 * k + 1] << 32) | d[8 + 2 * k];
+    // replay timers (10 ns ticks, k_tb_chain): [0] longest huge segment,
+    // [2] longest light phase of a block, [4] first block start -> last block end
+    for (auto& x : e->stats.stamp_cycles) x = 0;
+    e->stats.stamp_cycles[0] = d[8];
+    e->stats.stamp_cycles[2] = d[12];
+    if (d[13]) e->stats.stamp_cycles[4] = (uint32_t)(d[14] - ~d[13]);
     e->stats.stamp_cycles[6] = d[2];   // max rounds of one segment
     e->stats.last_heavy = c[0] + c[3];                        // chain (token-bucket) segments
     e->stats.last_segments = (uint64_t)c[0] + c[1] + c[2] + c[3];

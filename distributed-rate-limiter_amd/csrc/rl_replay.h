@@ -394,40 +394,65 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
 // requests in sorted order (one coalesced pass; random reads of the 28 B
 // request records, which stay in the Infinity Cache at 1M-request batches),
 // plus the token-bucket precomputation (TbPre)
+// One request as k_probe packs it in arrival order (server clock resolved):
+// the sorted-order gather of k_permute reads one 32-B record per request
+// instead of four scattered array elements.
+struct alignas(32) ReqRec {
+    int64_t ts, n, sms;
+    uint32_t cfg, pad;
+};
+
+// requests to sorted order + the state-free token-bucket precomputation.
+// Each wave covers 64 consecutive sorted positions; a request's predecessor
+// in its segment (position j-1) is the neighbouring lane's record, so only
+// lane 0 gathers a second one.
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
-                                                 const CfgDev* __restrict__ cfgs, int32_t profile, ReqArgs in,
-                                                 ReqArgs out, TbPre pre) {
-    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
-        const uint32_t k0 = sk[j];
-        if (k0 == invalid_key) continue;
-        const uint32_t i = sv[j];
-        const int64_t t = in.ts[i];
-        const uint32_t c = in.cfg[i];
-        const int64_t sms = in.sms ? in.sms[i] : floor_div(t, 1000000LL);
+                                                 const CfgDev* __restrict__ cfgs, int32_t profile,
+                                                 const ReqRec* __restrict__ rec, ReqArgs out, TbPre pre) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t j0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); j0 < m; j0 += gridDim.x * blockDim.x) {
+        const uint32_t j = j0 + lane;
+        const bool in = j < m;
+        const uint32_t k0 = in ? sk[j] : invalid_key;
+        const bool valid = k0 != invalid_key;
+        ReqRec r{};
+        if (valid) r = rec[sv[j]];
+        // predecessor (j-1) fields from the lane below
+        uint32_t kp = __shfl_up(k0, 1);
+        int64_t tp = __shfl_up(r.ts, 1);
+        int64_t smsp = __shfl_up(r.sms, 1);
+        uint32_t cp = __shfl_up(r.cfg, 1);
+        if (lane == 0) {
+            kp = invalid_key;
+            if (j > 0 && valid && k0 < win_base && sk[j - 1] == k0) {
+                const ReqRec q = rec[sv[j - 1]];
+                kp = k0;
+                tp = q.ts;
+                smsp = q.sms;
+                cp = q.cfg;
+            }
+        }
+        if (!valid) continue;
         // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
-        const_cast<int64_t*>(out.ts)[j] = t;
-        const_cast<int64_t*>(out.n)[j] = in.n[i];
-        const_cast<uint32_t*>(out.cfg)[j] = c;
-        const_cast<int64_t*>(out.sms)[j] = sms;
+        const_cast<int64_t*>(out.ts)[j] = r.ts;
+        const_cast<int64_t*>(out.n)[j] = r.n;
+        const_cast<uint32_t*>(out.cfg)[j] = r.cfg;
+        const_cast<int64_t*>(out.sms)[j] = r.sms;
         if (k0 >= win_base) continue;
-        const CfgDev& C = cfgs[c];
-        const double now = (double)t / 1e9;
+        const CfgDev& C = cfgs[r.cfg];
+        const double now = (double)r.ts / 1e9;
         // state-free: a head's add needs the table (tb_head_add, at replay)
         // and the table is still being updated by the previous batch
-        if (j > 0 && sk[j - 1] == k0) {
-            const uint32_t ip = sv[j - 1];
-            const int64_t tp = in.ts[ip];
-            const int64_t smsp = in.sms ? in.sms[ip] : floor_div(tp, 1000000LL);
+        if (kp == k0) {
             const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
-            const int64_t prev_when = expire_when(cfgs[in.cfg[ip]].ttl_tb, smsp);
-            pre.add[j] = key_alive(prev_when, sms, profile) ? (now - prev_last) * C.rate : __builtin_nan("");
+            const int64_t prev_when = expire_when(cfgs[cp].ttl_tb, smsp);
+            pre.add[j] = key_alive(prev_when, r.sms, profile) ? (now - prev_last) * C.rate : __builtin_nan("");
         }
-        const int64_t nv = in.n[i];
-        pre.th[j] = fmin(C.limit_d, (double)nv);
+        pre.th[j] = fmin(C.limit_d, (double)r.n);
         pre.reset[j] = tb_reset_at(now, C);
         pre.lq[j] = lua_tostring_roundtrip(now, profile);
-        pre.when[j] = expire_when(C.ttl_tb, sms);
+        pre.when[j] = expire_when(C.ttl_tb, r.sms);
     }
 }
 

@@ -84,9 +84,9 @@ typedef struct rl_stats {
     uint64_t last_coop_iters;  /* offset fixed-point iterations of the last batch (all heavy segments) */
     uint32_t sort_bits;
     uint32_t sort_passes;
-    uint64_t stamp_cycles[7];  /* replay timers of the last batch (10 ns ticks): [0] longest heavy segment,
-                                  [1] max per-block heavy phase, [2] max per-block light phase,
-                                  [3] max heavy segments per block, [6] max rounds of one segment */
+    uint64_t stamp_cycles[7];  /* replay timers of the last batch (10 ns ticks): [0] longest huge segment,
+                                  [2] max per-block light phase, [4] first block start to last block end,
+                                  [6] max rounds of one segment; [1] [3] [5] unused (0) */
     uint64_t coop_ends[4];     /* how the last batch's cooperative rounds ended: [0] window done,
                                   [1] stop request (allow / clamp / decade / expiry), [2] boundary
                                   (exact-pass mismatch safety net), [3] offset iteration cap */
