@@ -80,6 +80,26 @@ def cpu_baseline(workload, batch, sample):
                       f"(C restatement of Go+Redis Lua, glibc %.14g/strtod), single thread"}
 
 
+def e2e(args, out_fd):
+    """BASELINE configs[4] through the native load generator (a child process;
+    this process never touches the GPU)."""
+    import subprocess
+    exe = os.path.join(ROOT, "distributed-rate-limiter_amd", "lib", "rl_bench_e2e")
+    if not os.path.exists(exe):
+        raise SystemExit(f"{exe} not built (__graft_entry__.build())")
+    p = subprocess.run([exe, "--qps", args.qps, "--seconds", str(args.seconds)], stdout=subprocess.PIPE, check=True)
+    r = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    kept = [lv for lv in r["levels"] if lv["achieved_decisions_per_s"] >= 0.95 * lv["offered_qps"] and not lv["dropped"]]
+    top = kept[-1] if kept else r["levels"][0]
+    out = {"metric": "p99 decision latency at fixed offered QPS through the request coalescer (configs[4])",
+           "value": top["p99_us"], "unit": "us", "n_gpus": 1, "higher_is_better": False,
+           "vs_baseline": None, "dtype": "f64", "data": "synthetic (Zipf s=1.5 over 1M keys, Poisson arrivals)",
+           "config": {"workload": "configs[4]: Token Bucket 20/12s, 1M keys Zipf 1.5, open loop, coalesced batches",
+                      "value_at_qps": top["offered_qps"], "max_batch": r["max_batch"], "generators": r["gens"]},
+           "levels": r["levels"], "engine_status": r["engine_status"]}
+    os.write(out_fd, (json.dumps(out) + "\n").encode())
+
+
 def main():
     # one JSON line on stdout: anything native libraries print (the RCCL banner,
     # ROCm notices) goes to stderr; the line is written to the saved stdout
@@ -100,7 +120,14 @@ def main():
     ap.add_argument("--route", action="store_true",
                     help="routed ingress: every rank draws keys from the whole key space and an RCCL "
                          "all-to-all moves each request to its owner GPU and the result back")
+    ap.add_argument("--e2e", action="store_true",
+                    help="configs[4]: open-loop Zipf 1.5 traffic through the request coalescer at fixed QPS "
+                         "levels (lib/rl_bench_e2e); reports per-request latency percentiles")
+    ap.add_argument("--qps", default="1e5,1e6,1e7", help="--e2e offered QPS levels")
+    ap.add_argument("--seconds", type=float, default=2.0, help="--e2e seconds per QPS level")
     args = ap.parse_args()
+    if args.e2e:
+        return e2e(args, out_fd)
 
     import torch
     import torch.distributed as dist

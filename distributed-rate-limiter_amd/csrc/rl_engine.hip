@@ -55,6 +55,24 @@ __global__ void k_init_win(WinEntry* t, uint64_t n) {
 
 constexpr int PROBE_BLOCK = 256;
 
+// find-or-insert one request's key: its global slot (token-bucket table
+// first, then the window table at win_base), or invalid_key when the request
+// is not executed (n <= 0, unknown config, reserved key, table full)
+__device__ inline uint32_t probe_request(uint64_t k, uint32_t c, int64_t nn, const CfgDev* __restrict__ cfgs,
+                                         uint32_t ncfg, TbEntry* tb, uint64_t tb_mask, WinEntry* win,
+                                         uint64_t win_mask, uint32_t win_base, uint32_t invalid_key, uint32_t& ef) {
+    if (k == EMPTY_KEY) ef |= EF_BAD_KEY;
+    if (!(c < ncfg && nn > 0 && k != EMPTY_KEY)) return invalid_key;
+    if (cfgs[c].alg == ALG_TOKEN_BUCKET) {
+        const uint32_t s = probe_insert(tb, tb_mask, k);
+        if (s == NO_SLOT) { ef |= EF_TABLE_FULL; return invalid_key; }
+        return s;
+    }
+    const uint32_t s = probe_insert(win, win_mask, k);
+    if (s == NO_SLOT) { ef |= EF_TABLE_FULL; return invalid_key; }
+    return win_base + s;
+}
+
 // find-or-insert every request's key; sort key = global slot id; fused
 // per-pass digit histograms (LDS, then one global atomic per bin per block)
 __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
@@ -68,22 +86,11 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     __syncthreads();
     uint32_t ef = 0;
     for (uint32_t i = blockIdx.x * PROBE_BLOCK + threadIdx.x; i < m; i += gridDim.x * PROBE_BLOCK) {
-        uint64_t k = key[i];
-        uint32_t c = cfg[i];
-        int64_t nn = n[i];
-        uint32_t slot = invalid_key;
-        bool ok = c < ncfg && nn > 0 && k != EMPTY_KEY;
-        if (k == EMPTY_KEY) ef |= EF_BAD_KEY;
-        if (ok) {
-            int32_t alg = cfgs[c].alg;
-            if (alg == ALG_TOKEN_BUCKET) {
-                uint32_t s = probe_insert(tb, tb_mask, k);
-                if (s == NO_SLOT) ef |= EF_TABLE_FULL; else slot = s;
-            } else {
-                uint32_t s = probe_insert(win, win_mask, k);
-                if (s == NO_SLOT) ef |= EF_TABLE_FULL; else slot = win_base + s;
-            }
-        }
+        const uint64_t k = key[i];
+        const uint32_t c = cfg[i];
+        const int64_t nn = n[i];
+        const uint32_t slot = probe_request(k, c, nn, cfgs, ncfg, tb, tb_mask, win, win_mask, win_base,
+                                            invalid_key, ef);
         sk[i] = slot;
         // one 32-B record per request: k_permute's sorted-order gather then
         // touches one line fragment instead of four arrays
@@ -103,6 +110,148 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
         uint32_t v = lh[p][threadIdx.x];
         if (v) atomicAdd(&ghist[p * RADIX + threadIdx.x], v);
     }
+}
+
+// Small batches (m <= SMALL_MAX): the whole launch sequence in one workgroup
+// and one launch -- find-or-insert, a bitonic sort of (slot, arrival index) in
+// LDS, the sorted-order copy with the state-free token-bucket precomputation
+// (as k_permute), one thread per key segment replaying it serially
+// (replay_tb_serial / replay_win_serial, the big path's exact fallbacks), and
+// the results in the caller's order (as k_unpermute).  A request-coalescing
+// server at moderate load sends batches of a few to a few thousand requests;
+// for them the big path's ten launches on three streams cost more than the
+// work.  Same semantics, same table: batches of either size may interleave.
+constexpr int SMALL_BLOCK = 1024;
+constexpr uint32_t SMALL_MAX = 4096;
+
+__global__ __launch_bounds__(SMALL_BLOCK) void k_small(
+    uint32_t m, ReqArgs in, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb, uint64_t tb_mask,
+    WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key, int32_t profile, ReqArgs ps,
+    TbPre pre, uint32_t heavy_min, uint32_t* eflags) {
+    __shared__ uint64_t sk[SMALL_MAX];   // (slot << 32) | arrival index
+    __shared__ uint64_t heavy[SMALL_MAX / 32];   // (end << 32) | start of each long segment
+    __shared__ uint32_t nheavy;
+    if (threadIdx.x == 0) nheavy = 0;
+    uint32_t P = 64;
+    while (P < m) P <<= 1;
+    uint32_t ef = 0;
+    for (uint32_t i = threadIdx.x; i < P; i += SMALL_BLOCK) {
+        uint64_t v = ~0ull;
+        if (i < m) {
+            const uint32_t slot = probe_request(in.key[i], in.cfg[i], in.n[i], cfgs, ncfg, tb, tb_mask, win,
+                                                win_mask, win_base, invalid_key, ef);
+            v = ((uint64_t)slot << 32) | i;
+        }
+        sk[i] = v;
+    }
+    __syncthreads();
+    // bitonic sort, ascending: the keys are unique (the index is in the low bits)
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += SMALL_BLOCK) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = sk[i], b = sk[l];
+                    if ((a > b) == ((i & k) == 0)) { sk[i] = b; sk[l] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // sorted-order copy + token-bucket precomputation (k_permute)
+    for (uint32_t j = threadIdx.x; j < m; j += SMALL_BLOCK) {
+        const uint32_t k0 = (uint32_t)(sk[j] >> 32);
+        if (k0 == invalid_key) continue;
+        const uint32_t i = (uint32_t)sk[j];
+        const int64_t t = in.ts[i];
+        const uint32_t c = in.cfg[i];
+        const int64_t sms = in.sms ? in.sms[i] : floor_div(t, 1000000LL);
+        const int64_t nv = in.n[i];
+        const_cast<int64_t*>(ps.ts)[j] = t;
+        const_cast<int64_t*>(ps.n)[j] = nv;
+        const_cast<uint32_t*>(ps.cfg)[j] = c;
+        const_cast<int64_t*>(ps.sms)[j] = sms;
+        if (k0 >= win_base) continue;
+        const CfgDev& C = cfgs[c];
+        const double now = (double)t / 1e9;
+        if (j > 0 && (uint32_t)(sk[j - 1] >> 32) == k0) {
+            const uint32_t ip = (uint32_t)sk[j - 1];
+            const int64_t tp = in.ts[ip];
+            const int64_t smsp = in.sms ? in.sms[ip] : floor_div(tp, 1000000LL);
+            const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
+            const int64_t prev_when = expire_when(cfgs[in.cfg[ip]].ttl_tb, smsp);
+            pre.add[j] = key_alive(prev_when, sms, profile) ? (now - prev_last) * C.rate : __builtin_nan("");
+        }
+        pre.th[j] = fmin(C.limit_d, (double)nv);
+        pre.reset[j] = tb_reset_at(now, C);
+        pre.lq[j] = lua_tostring_roundtrip(now, profile);
+        pre.when[j] = expire_when(C.ttl_tb, sms);
+    }
+    __syncthreads();
+    // segments: short ones replay serially, one thread each (exact fallbacks
+    // of the big path); segments of heavy_min or more go to a list that the
+    // waves replay cooperatively (wave_segment / wave_win_segment, the big
+    // path's per-wave heavy replay)
+    for (uint32_t j = threadIdx.x; j < m; j += SMALL_BLOCK) {
+        const uint32_t k0 = (uint32_t)(sk[j] >> 32);
+        if (k0 == invalid_key || (j > 0 && (uint32_t)(sk[j - 1] >> 32) == k0)) continue;
+        // end of the segment: galloping search in LDS
+        uint32_t lo = j, step = 1;
+        while (lo + step < m && (uint32_t)(sk[lo + step] >> 32) == k0) { lo += step; step <<= 1; }
+        uint32_t hi = lo + step < m ? lo + step : m;
+        while (hi - lo > 1) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if ((uint32_t)(sk[mid] >> 32) == k0) lo = mid; else hi = mid;
+        }
+        const uint32_t j1 = lo + 1;
+        if (j1 - j >= heavy_min) {
+            const uint32_t h = atomicAdd(&nheavy, 1u);
+            heavy[h] = ((uint64_t)j1 << 32) | j;
+            continue;
+        }
+        if (k0 < win_base) replay_tb_serial(&tb[k0], j, j1, cfgs, profile, ps, pre);
+        else replay_win_serial(&win[k0 - win_base], j, j1, cfgs, profile, ps, eflags);
+    }
+    __syncthreads();
+    {
+        const uint32_t nh = nheavy;
+        uint32_t iters = 0;
+        for (uint32_t h = threadIdx.x >> 6; h < nh; h += SMALL_BLOCK / 64) {
+            const uint32_t j0 = (uint32_t)heavy[h], j1 = (uint32_t)(heavy[h] >> 32);
+            const uint32_t k0 = (uint32_t)(sk[j0] >> 32);
+            if (k0 < win_base) wave_segment(&tb[k0], j0, j1, cfgs, profile, ps, pre, eflags, iters);
+            else wave_win_segment(&win[k0 - win_base], j0, j1, cfgs, profile, ps, eflags);
+        }
+    }
+    __syncthreads();
+    // results to the caller's order (k_unpermute)
+    for (uint32_t j = threadIdx.x; j < m; j += SMALL_BLOCK) {
+        const uint32_t k0 = (uint32_t)(sk[j] >> 32);
+        const uint32_t i = (uint32_t)sk[j];
+        if (k0 == invalid_key) {
+            in.dec[i] = DEC_INVALID;
+            in.rem[i] = 0;
+            in.retry[i] = 0;
+            in.reset[i] = 0;
+            if (in.tok) in.tok[i] = 0.0;
+            continue;
+        }
+        const uint8_t dec = ps.dec[j];
+        const double tok = ps.tok[j];
+        int64_t rem, retry;
+        if (k0 < win_base) {
+            tb_result(dec, tok, ps.n[j], cfgs[ps.cfg[j]], rem, retry);
+        } else {
+            rem = ps.rem[j];
+            retry = ps.retry[j];
+        }
+        in.dec[i] = dec;
+        in.rem[i] = rem;
+        in.retry[i] = retry;
+        in.reset[i] = ps.reset[j];
+        if (in.tok) in.tok[i] = tok;
+    }
+    if (ef) atomicOr(eflags, ef);
 }
 
 // Reset: DEL of the key(s) AllowN would touch at ts (tokenbucket.go:136-144,
@@ -225,6 +374,16 @@ struct rl_engine {
     uint32_t max_batch = 0;
     uint32_t max_tiles = 0;
     BatchSet set[NSETS];
+    // k_small: batches up to small_max run as one workgroup on `chain`; its
+    // sorted-order scratch (reused by consecutive small batches, which the
+    // chain stream orders)
+    uint32_t small_max = 0;
+    int64_t *s_ts = nullptr, *s_n = nullptr, *s_sms = nullptr, *s_rem = nullptr, *s_retry = nullptr,
+            *s_reset = nullptr, *s_when = nullptr;
+    uint32_t* s_cfg = nullptr;
+    uint8_t* s_dec = nullptr;
+    double *s_tok = nullptr, *s_add = nullptr, *s_lq = nullptr, *s_th = nullptr;
+    hipEvent_t ev_small = nullptr;
     int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
     size_t zero_bytes = 0;
     int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
@@ -337,6 +496,11 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_dec); (void)hipFree(e->d_rem); (void)hipFree(e->d_retry); (void)hipFree(e->d_reset); (void)hipFree(e->d_tok);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->ev_in) (void)hipEventDestroy(e->ev_in);
+    if (e->ev_small) (void)hipEventDestroy(e->ev_small);
+    for (void* p : {(void*)e->s_ts, (void*)e->s_n, (void*)e->s_sms, (void*)e->s_rem, (void*)e->s_retry,
+                    (void*)e->s_reset, (void*)e->s_when, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
+                    (void*)e->s_add, (void*)e->s_lq, (void*)e->s_th})
+        (void)hipFree(p);
     if (e->front) (void)hipStreamDestroy(e->front);
     if (e->chain) (void)hipStreamDestroy(e->chain);
     if (e->tail) (void)hipStreamDestroy(e->tail);
@@ -353,6 +517,8 @@ static int drain(rl_engine* e) {
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return RL_OK;
 }
+
+static int warm_up(rl_engine* e);
 
 extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (!o || !out) return RL_EINVAL;
@@ -399,6 +565,9 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     }
     e->stream = e->tail;
     if (hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipEventCreateWithFlags(&e->ev_small, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
+    e->small_max = SMALL_MAX;
+    if (const char* v = getenv("RL_SMALL_MAX")) e->small_max = std::min<uint32_t>((uint32_t)atoi(v), SMALL_MAX);
     size_t M = e->max_batch;
     e->cfg_cap = 64;
     const size_t status_words = (size_t)4 * e->max_tiles * RADIX;
@@ -419,6 +588,12 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_retry, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_tok, 8 * M) == hipSuccess;
+    for (int64_t** p : {&e->s_ts, &e->s_n, &e->s_sms, &e->s_rem, &e->s_retry, &e->s_reset, &e->s_when})
+        ok &= hipMalloc(p, 8 * SMALL_MAX) == hipSuccess;
+    // add / th: 128 elements of slack, as the batch sets' (exact_span reads ahead)
+    for (double** p : {&e->s_tok, &e->s_add, &e->s_lq, &e->s_th}) ok &= hipMalloc(p, 8 * (SMALL_MAX + 128)) == hipSuccess;
+    ok &= hipMalloc(&e->s_cfg, 4 * SMALL_MAX) == hipSuccess;
+    ok &= hipMalloc(&e->s_dec, SMALL_MAX) == hipSuccess;
     if (!ok) return bail(RL_ENOMEM);
     k_init_tb<<<2048, 256, 0, e->stream>>>(e->d_tb, e->tb_cap);
     k_init_win<<<2048, 256, 0, e->stream>>>(e->d_win, e->win_cap);
@@ -444,6 +619,10 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     }
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
+    {
+        const int r = warm_up(e);
+        if (r != RL_OK) return bail(r);
+    }
     *out = e;
     return RL_OK;
 }
@@ -501,8 +680,28 @@ static hipEvent_t take_event(rl_engine* e) {
 // enqueue one batch of m <= max_batch requests (see BatchSet); s waits for
 // its finish.  inputs_ready: the caller guarantees the input arrays are
 // complete now (RL_OPT_PIPELINE); otherwise the grouping waits for s.
+static int run_small(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, bool inputs_ready) {
+    hipStream_t c = e->chain;   // after every earlier replay (table state)
+    if (!inputs_ready) {
+        HIPCHK(e, hipEventRecord(e->ev_in, s));
+        HIPCHK(e, hipStreamWaitEvent(c, e->ev_in, 0));
+    }
+    ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, e->s_sms, e->s_dec, e->s_rem, e->s_retry, e->s_reset, e->s_tok};
+    TbPre pre{e->s_add, e->s_th, e->s_reset, e->s_lq, e->s_when};
+    k_small<<<1, SMALL_BLOCK, 0, c>>>(m, a, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
+                                      e->win_cap - 1, e->win_base, e->invalid_key, e->profile, ps, pre,
+                                      std::max<uint32_t>(e->heavy_min, 32), e->d_eflags);
+    HIPCHK(e, hipEventRecord(e->ev_small, c));
+    HIPCHK(e, hipStreamWaitEvent(s, e->ev_small, 0));
+    HIPCHK(e, hipGetLastError());
+    e->stats.batches++;
+    e->stats.decisions += m;
+    return RL_OK;
+}
+
 static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, bool inputs_ready) {
     if (m == 0) return RL_OK;
+    if (m <= e->small_max && !e->timing) return run_small(e, m, a, s, inputs_ready);
     BatchSet& B = e->set[e->next_set];
     e->last_set = e->next_set;
     e->next_set = (e->next_set + 1) % NSETS;
@@ -592,6 +791,31 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     HIPCHK(e, hipGetLastError());
     e->stats.batches++;
     e->stats.decisions += m;
+    return RL_OK;
+}
+
+// Launch every kernel once at creation, on batches of requests that are all
+// rejected (no config is registered yet), so no table entry is touched: HIP
+// loads kernels lazily, and a server's first batch on either path (k_small, or
+// the big path when load grows) would otherwise stall its queue for the load.
+static int warm_up(rl_engine* e) {
+    const uint32_t mb = std::min<uint32_t>(e->max_batch, e->small_max + 1);
+    hipStream_t s = e->stream;
+    HIPCHK(e, hipMemsetAsync(e->d_key, 0, 8 * (size_t)mb, s));
+    HIPCHK(e, hipMemsetAsync(e->d_n, 0, 8 * (size_t)mb, s));
+    HIPCHK(e, hipMemsetAsync(e->d_ts, 0, 8 * (size_t)mb, s));
+    HIPCHK(e, hipMemsetAsync(e->d_cfgid, 0, 4 * (size_t)mb, s));
+    ReqArgs a{e->d_key, e->d_ts, e->d_n, e->d_cfgid, nullptr, e->d_dec, e->d_rem, e->d_retry, e->d_reset, e->d_tok};
+    for (uint32_t m : {1u, mb}) {
+        const int r = run_batch(e, m, a, s, false);
+        if (r != RL_OK) return r;
+    }
+    const int r = drain(e);
+    if (r != RL_OK) return r;
+    HIPCHK(e, hipMemset(e->d_eflags, 0, 4));
+    e->stats = rl_stats{};
+    e->stats.sort_bits = e->sort_bits;
+    e->stats.sort_passes = e->sort_passes;
     return RL_OK;
 }
 

@@ -1,0 +1,426 @@
+// coalescer.cpp -- see coalescer.hpp / include/rl_coalescer.h.
+#include "coalescer.hpp"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+
+namespace rlc {
+
+int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// per request: key 8 + ts 8 + n 8 + rem 8 + retry 8 + reset 8 + cfg 4 + dec 1
+Sub::Sub(size_t m_) : m(m_), left(m_), mem(new uint8_t[m_ * 53 + 8]) {
+    uint8_t* p = mem.get();
+    key = reinterpret_cast<uint64_t*>(p);
+    ts = reinterpret_cast<int64_t*>(p + 8 * m);
+    n = reinterpret_cast<int64_t*>(p + 16 * m);
+    rem = reinterpret_cast<int64_t*>(p + 24 * m);
+    retry = reinterpret_cast<int64_t*>(p + 32 * m);
+    reset = reinterpret_cast<int64_t*>(p + 40 * m);
+    cfg = reinterpret_cast<uint32_t*>(p + 48 * m);
+    dec = p + 52 * m;
+}
+
+// ---------------------------------------------------------------------------
+// GPU backend: pinned staging per slot, one H2D copy stream, results come back
+// on an output stream that the engine orders behind each batch's finish.
+// Inputs are complete when rl_decide_batch_device is called (the H2D copy is
+// waited for on the submitter thread), so an engine created with
+// RL_OPT_PIPELINE overlaps batch b+1's grouping with batch b's replay.
+// ---------------------------------------------------------------------------
+class GpuBackend : public Backend {
+public:
+    explicit GpuBackend(rl_engine* e) : e_(e) { (void)hipGetDevice(&dev_id_); }
+    ~GpuBackend() override {
+        for (auto& d : dev_) {
+            (void)hipFree(d.key);
+            if (d.ev) (void)hipEventDestroy(d.ev);
+        }
+        for (void* h : host_) (void)hipHostFree(h);
+        if (cs_) (void)hipStreamDestroy(cs_);
+        if (os_) (void)hipStreamDestroy(os_);
+    }
+    int init(int nslots, size_t M, std::vector<Slot>* slots) override {
+        (void)hipSetDevice(dev_id_);
+        if (hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking) != hipSuccess) return RL_EDEVICE;
+        if (hipStreamCreateWithFlags(&os_, hipStreamNonBlocking) != hipSuccess) return RL_EDEVICE;
+        slots->resize(nslots);
+        dev_.resize(nslots);
+        for (int i = 0; i < nslots; i++) {
+            // inputs first (one H2D block), then outputs
+            void* h = nullptr;
+            if (hipHostMalloc(&h, M * 61 + 64, hipHostMallocDefault) != hipSuccess) return RL_ENOMEM;
+            host_.push_back(h);
+            carve(static_cast<uint8_t*>(h), M, (*slots)[i]);
+            Dev& d = dev_[i];
+            uint8_t* dp = nullptr;
+            if (hipMalloc(&dp, M * 61 + 64) != hipSuccess) return RL_ENOMEM;
+            d.key = dp;
+            if (hipEventCreateWithFlags(&d.ev, hipEventDisableTiming) != hipSuccess) return RL_EDEVICE;
+        }
+        M_ = M;
+        return RL_OK;
+    }
+    int launch(int i, Slot& s) override {
+        (void)hipSetDevice(dev_id_);   // the submitter thread
+        Dev& d = dev_[i];
+        Slot dv;
+        carve(d.key, M_, dv);
+        const size_t m = s.m;
+        bool ok = hipMemcpyAsync(dv.key, s.key, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
+        ok &= hipMemcpyAsync(dv.ts, s.ts, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
+        ok &= hipMemcpyAsync(dv.n, s.n, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
+        ok &= hipMemcpyAsync(dv.cfg, s.cfg, 4 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
+        ok &= hipStreamSynchronize(cs_) == hipSuccess;
+        if (!ok) return RL_EDEVICE;
+        int rc = rl_decide_batch_device(e_, m, dv.key, dv.ts, dv.n, dv.cfg, nullptr, dv.dec, dv.rem, dv.retry,
+                                        dv.reset, nullptr, os_);
+        if (rc != RL_OK) return rc;
+        ok = hipMemcpyAsync(s.dec, dv.dec, m, hipMemcpyDeviceToHost, os_) == hipSuccess;
+        ok &= hipMemcpyAsync(s.rem, dv.rem, 8 * m, hipMemcpyDeviceToHost, os_) == hipSuccess;
+        ok &= hipMemcpyAsync(s.retry, dv.retry, 8 * m, hipMemcpyDeviceToHost, os_) == hipSuccess;
+        ok &= hipMemcpyAsync(s.reset, dv.reset, 8 * m, hipMemcpyDeviceToHost, os_) == hipSuccess;
+        ok &= hipEventRecord(d.ev, os_) == hipSuccess;
+        return ok ? RL_OK : RL_EDEVICE;
+    }
+    int wait(int i, Slot&) override {
+        (void)hipSetDevice(dev_id_);   // the completer thread
+        return hipEventSynchronize(dev_[i].ev) == hipSuccess ? RL_OK : RL_EDEVICE;
+    }
+
+private:
+    struct Dev {
+        uint8_t* key = nullptr;   // base of the slot's device block
+        hipEvent_t ev = nullptr;
+    };
+    // SoA layout of one slot block: key ts n | cfg | rem retry reset | dec
+    static void carve(uint8_t* p, size_t M, Slot& s) {
+        s.key = reinterpret_cast<uint64_t*>(p);
+        s.ts = reinterpret_cast<int64_t*>(p + 8 * M);
+        s.n = reinterpret_cast<int64_t*>(p + 16 * M);
+        s.cfg = reinterpret_cast<uint32_t*>(p + 24 * M);
+        uint8_t* q = p + ((28 * M + 63) & ~size_t(63));
+        s.rem = reinterpret_cast<int64_t*>(q);
+        s.retry = reinterpret_cast<int64_t*>(q + 8 * M);
+        s.reset = reinterpret_cast<int64_t*>(q + 16 * M);
+        s.dec = q + 24 * M;
+    }
+    rl_engine* e_;
+    int dev_id_ = 0;             // the engine's device: current when the coalescer is created
+    hipStream_t cs_ = nullptr, os_ = nullptr;
+    std::vector<void*> host_;
+    std::vector<Dev> dev_;
+    size_t M_ = 0;
+};
+
+// synchronous host function (the CPU tests plug the oracle in here)
+class FnBackend : public Backend {
+public:
+    FnBackend(rl_batch_fn fn, void* user) : fn_(fn), user_(user) {}
+    int init(int nslots, size_t M, std::vector<Slot>* slots) override {
+        slots->resize(nslots);
+        mem_.resize(nslots);
+        for (int i = 0; i < nslots; i++) {
+            mem_[i].reset(new uint8_t[M * 61 + 64]);
+            uint8_t* p = mem_[i].get();
+            Slot& s = (*slots)[i];
+            s.key = reinterpret_cast<uint64_t*>(p);
+            s.ts = reinterpret_cast<int64_t*>(p + 8 * M);
+            s.n = reinterpret_cast<int64_t*>(p + 16 * M);
+            s.rem = reinterpret_cast<int64_t*>(p + 24 * M);
+            s.retry = reinterpret_cast<int64_t*>(p + 32 * M);
+            s.reset = reinterpret_cast<int64_t*>(p + 40 * M);
+            s.cfg = reinterpret_cast<uint32_t*>(p + 48 * M);
+            s.dec = p + 52 * M;
+        }
+        return RL_OK;
+    }
+    int launch(int, Slot& s) override {
+        return fn_(user_, s.m, s.key, s.ts, s.n, s.cfg, s.dec, s.rem, s.retry, s.reset);
+    }
+    int wait(int, Slot&) override { return RL_OK; }
+
+private:
+    rl_batch_fn fn_;
+    void* user_;
+    std::vector<std::unique_ptr<uint8_t[]>> mem_;
+};
+
+std::unique_ptr<Backend> make_gpu_backend(rl_engine* e) { return std::unique_ptr<Backend>(new GpuBackend(e)); }
+std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, void* user) {
+    return std::unique_ptr<Backend>(new FnBackend(fn, user));
+}
+
+// ---------------------------------------------------------------------------
+
+Coalescer::Coalescer(std::unique_ptr<Backend> be, const rl_coalescer_opts& o) : be_(std::move(be)), o_(o) {
+    if (o_.max_batch == 0) o_.max_batch = 65536;
+    if (o_.max_in_flight == 0) o_.max_in_flight = 3;
+    if (o_.max_in_flight > 3) o_.max_in_flight = 3;
+    if (o_.queue_cap == 0) o_.queue_cap = 1ull << 24;
+    if (o_.linger_ns < 0) o_.linger_ns = 0;
+}
+
+int Coalescer::start() {
+    int rc = be_->init((int)o_.max_in_flight, o_.max_batch, &slots_);
+    if (rc != RL_OK) return rc;
+    t_sub_ = std::thread([this] { submitter(); });
+    t_done_ = std::thread([this] { completer(); });
+    return RL_OK;
+}
+
+Coalescer::~Coalescer() {
+    Shutdown();
+    for (auto& kv : subs_) delete kv.second;
+}
+
+void Coalescer::Shutdown() {
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (stop_) return;
+        stop_ = true;
+    }
+    cv_sub_.notify_all();
+    cv_done_.notify_all();
+    if (t_sub_.joinable()) t_sub_.join();
+    if (t_done_.joinable()) t_done_.join();
+    // anything never launched (backend failure) is released as closed
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto& kv : subs_) {
+        Sub* s = kv.second;
+        if (!s->done) {
+            s->done = true;
+            s->status = RL_ECLOSED;
+            s->cv.notify_all();
+        }
+    }
+}
+
+int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
+                      uint64_t* ticket) {
+    if (!ticket || (m && (!key || !ts || !n || !cfg))) return RL_EINVAL;
+    Sub* s = new Sub(m);
+    memcpy(s->key, key, 8 * m);
+    memcpy(s->ts, ts, 8 * m);
+    memcpy(s->n, n, 8 * m);
+    memcpy(s->cfg, cfg, 4 * m);
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (stop_) {
+            delete s;
+            return RL_ECLOSED;
+        }
+        if (pending_ + m > o_.queue_cap) {
+            delete s;
+            return RL_EAGAIN;
+        }
+        s->first = next_seq_;
+        // an empty submission is done at once; its ticket must still be unique
+        next_seq_ += m ? m : 1;
+        subs_[s->first] = s;
+        st_.submitted += m;
+        if (m) {
+            queue_.push_back(s);
+            pending_ += m;
+        } else {
+            s->done = true;
+            s->done_ns = steady_ns();
+        }
+        *ticket = s->first;
+    }
+    if (m) cv_sub_.notify_one();
+    return RL_OK;
+}
+
+int Coalescer::Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* rem, int64_t* retry,
+                    int64_t* reset, int64_t* done_ns) {
+    std::unique_lock<std::mutex> lk(mu_);
+    auto it = subs_.find(ticket);
+    if (it == subs_.end()) return RL_EINVAL;
+    Sub* s = it->second;
+    if (timeout_ns < 0) {
+        s->cv.wait(lk, [&] { return s->done; });
+    } else if (!s->cv.wait_for(lk, std::chrono::nanoseconds(timeout_ns), [&] { return s->done; })) {
+        return RL_ETIMEOUT;
+    }
+    subs_.erase(it);
+    lk.unlock();
+    const size_t m = s->m;
+    if (dec) memcpy(dec, s->dec, m);
+    if (rem) memcpy(rem, s->rem, 8 * m);
+    if (retry) memcpy(retry, s->retry, 8 * m);
+    if (reset) memcpy(reset, s->reset, 8 * m);
+    if (done_ns) *done_ns = s->done_ns;
+    int st = s->status;
+    delete s;
+    return st;
+}
+
+rl_coalescer_stats Coalescer::Stats() {
+    std::lock_guard<std::mutex> g(mu_);
+    rl_coalescer_stats r = st_;
+    r.pending = pending_;
+    return r;
+}
+
+void Coalescer::submitter() {
+    for (;;) {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_sub_.wait(lk, [&] { return (stop_ && pending_ == 0) || (pending_ > 0 && inflight_ < (int)o_.max_in_flight); });
+        if (pending_ == 0) break;   // stop_ with nothing left
+        if (o_.linger_ns > 0 && inflight_ == 0 && pending_ < o_.max_batch && !stop_) {
+            const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(o_.linger_ns);
+            cv_sub_.wait_until(lk, until, [&] { return stop_ || pending_ >= o_.max_batch; });
+        }
+        const int si = next_slot_;
+        next_slot_ = (next_slot_ + 1) % (int)o_.max_in_flight;
+        Slot& s = slots_[si];
+        s.parts.clear();
+        size_t m = 0;
+        while (m < o_.max_batch && !queue_.empty()) {
+            Sub* sub = queue_.front();
+            const size_t take = std::min(sub->m - sub->taken, (size_t)o_.max_batch - m);
+            s.parts.push_back({sub, sub->taken, take, m});
+            sub->taken += take;
+            m += take;
+            if (sub->taken == sub->m) queue_.pop_front();
+        }
+        pending_ -= m;
+        inflight_++;
+        lk.unlock();
+        // the submissions' inputs are immutable after Submit: copy unlocked
+        for (const auto& p : s.parts) {
+            memcpy(s.key + p.at, p.sub->key + p.off, 8 * p.count);
+            memcpy(s.ts + p.at, p.sub->ts + p.off, 8 * p.count);
+            memcpy(s.n + p.at, p.sub->n + p.off, 8 * p.count);
+            memcpy(s.cfg + p.at, p.sub->cfg + p.off, 4 * p.count);
+        }
+        s.m = m;
+        s.status = be_->launch(si, s);
+        lk.lock();
+        st_.batches++;
+        st_.max_batch_seen = std::max<uint64_t>(st_.max_batch_seen, m);
+        launched_.push_back(si);
+        lk.unlock();
+        cv_done_.notify_one();
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    sub_exited_ = true;
+    cv_done_.notify_all();
+}
+
+void Coalescer::completer() {
+    for (;;) {
+        int si;
+        {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_done_.wait(lk, [&] { return !launched_.empty() || sub_exited_; });
+            if (launched_.empty()) break;
+            si = launched_.front();
+        }
+        Slot& s = slots_[si];
+        int st = s.status == RL_OK ? be_->wait(si, s) : s.status;
+        for (const auto& p : s.parts) {
+            memcpy(p.sub->dec + p.off, s.dec + p.at, p.count);
+            memcpy(p.sub->rem + p.off, s.rem + p.at, 8 * p.count);
+            memcpy(p.sub->retry + p.off, s.retry + p.at, 8 * p.count);
+            memcpy(p.sub->reset + p.off, s.reset + p.at, 8 * p.count);
+        }
+        const int64_t now = steady_ns();
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            launched_.pop_front();
+            inflight_--;
+            st_.decided += s.m;
+            for (const auto& p : s.parts) {
+                Sub* sub = p.sub;
+                if (st != RL_OK) sub->status = st;
+                sub->left -= p.count;
+                if (sub->left == 0) {
+                    sub->done = true;
+                    sub->done_ns = now;
+                    sub->cv.notify_all();
+                }
+            }
+        }
+        cv_sub_.notify_one();
+    }
+}
+
+}  // namespace rlc
+
+// ---------------------------------------------------------------------------
+// C-ABI
+// ---------------------------------------------------------------------------
+
+struct rl_coalescer {
+    rlc::Coalescer* c;
+};
+
+rlc::Coalescer* rlc::unwrap(rl_coalescer* c) { return c ? c->c : nullptr; }
+
+static int create(std::unique_ptr<rlc::Backend> be, const rl_coalescer_opts* opts, rl_coalescer** out) {
+    rl_coalescer_opts o{};
+    if (opts) o = *opts;
+    auto* c = new rlc::Coalescer(std::move(be), o);
+    int rc = c->start();
+    if (rc != RL_OK) {
+        delete c;
+        return rc;
+    }
+    *out = new rl_coalescer{c};
+    return RL_OK;
+}
+
+extern "C" int rl_coalescer_create(rl_engine* e, const rl_coalescer_opts* opts, rl_coalescer** out) {
+    if (!e || !out) return RL_EINVAL;
+    return create(rlc::make_gpu_backend(e), opts, out);
+}
+
+extern "C" int rl_coalescer_create_with_backend(rl_batch_fn fn, void* user, const rl_coalescer_opts* opts,
+                                                rl_coalescer** out) {
+    if (!fn || !out) return RL_EINVAL;
+    return create(rlc::make_fn_backend(fn, user), opts, out);
+}
+
+extern "C" int rl_coalescer_destroy(rl_coalescer* c) {
+    if (!c) return RL_EINVAL;
+    delete c->c;
+    delete c;
+    return RL_OK;
+}
+
+extern "C" int rl_coalescer_submit(rl_coalescer* c, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
+                                   const int64_t* n, const uint32_t* cfg_id, uint64_t* ticket) {
+    if (!c) return RL_EINVAL;
+    return c->c->Submit(m, key_id, ts_ns, n, cfg_id, ticket);
+}
+
+extern "C" int rl_coalescer_wait(rl_coalescer* c, uint64_t ticket, int64_t timeout_ns, uint8_t* decision,
+                                 int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns) {
+    if (!c) return RL_EINVAL;
+    return c->c->Wait(ticket, timeout_ns, decision, remaining, retry_after_ns, reset_at_ns);
+}
+
+extern "C" int rl_coalescer_decide(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, int64_t n, uint32_t cfg_id,
+                                   uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                                   int64_t* reset_at_ns) {
+    if (!c) return RL_EINVAL;
+    uint64_t t;
+    int rc = c->c->Submit(1, &key_id, &ts_ns, &n, &cfg_id, &t);
+    if (rc != RL_OK) return rc;
+    return c->c->Wait(t, -1, decision, remaining, retry_after_ns, reset_at_ns);
+}
+
+extern "C" int rl_coalescer_get_stats(rl_coalescer* c, rl_coalescer_stats* out) {
+    if (!c || !out) return RL_EINVAL;
+    *out = c->c->Stats();
+    return RL_OK;
+}

@@ -1,0 +1,110 @@
+// coalescer.hpp -- request coalescer in front of the decision engine
+// (include/rl_coalescer.h has the policy and ordering contract).
+//
+// The reference's Limiter.AllowN is one Redis EVAL per call
+// (tokenbucket.go:172, slidingwindow.go:164, fixedwindow.go:152); the north
+// star's BatchAllow path gathers concurrent calls into GPU batches
+// (SURVEY.md §8b, §8f rank 1).  Threads: callers submit and wait; one
+// submitter thread forms batches and launches them; one completer thread
+// waits for each launch in order and hands results back.
+#pragma once
+
+#include <stdint.h>
+
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/rl_coalescer.h"
+
+namespace rlc {
+
+// one launch's staging buffers (host side; pinned for the GPU backend)
+struct Slot {
+    uint64_t* key = nullptr;
+    int64_t* ts = nullptr;
+    int64_t* n = nullptr;
+    uint32_t* cfg = nullptr;
+    uint8_t* dec = nullptr;
+    int64_t* rem = nullptr;
+    int64_t* retry = nullptr;
+    int64_t* reset = nullptr;
+    size_t m = 0;
+    int status = RL_OK;
+    struct Part {
+        struct Sub* sub;
+        size_t off, count, at;   // sub[off, off+count) <-> slot[at, at+count)
+    };
+    std::vector<Part> parts;
+};
+
+// where batches go: the GPU engine, or a synchronous host function (tests)
+class Backend {
+public:
+    virtual ~Backend() = default;
+    virtual int init(int nslots, size_t max_batch, std::vector<Slot>* slots) = 0;
+    virtual int launch(int slot, Slot& s) = 0;   // asynchronous
+    virtual int wait(int slot, Slot& s) = 0;     // until launch `slot` completed
+};
+
+std::unique_ptr<Backend> make_gpu_backend(rl_engine* e);
+std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, void* user);
+
+// one submission: its requests (copied) and results
+struct Sub {
+    uint64_t first = 0;
+    size_t m = 0, taken = 0, left = 0;
+    int status = RL_OK;
+    bool done = false;
+    int64_t done_ns = 0;          // steady clock at completion
+    std::condition_variable cv;
+    std::unique_ptr<uint8_t[]> mem;
+    uint64_t* key;
+    int64_t *ts, *n, *rem, *retry, *reset;
+    uint32_t* cfg;
+    uint8_t* dec;
+    explicit Sub(size_t m);
+};
+
+int64_t steady_ns();
+
+class Coalescer {
+public:
+    Coalescer(std::unique_ptr<Backend> be, const rl_coalescer_opts& o);
+    ~Coalescer();
+    int start();
+    int Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
+               uint64_t* ticket);
+    // done_ns (optional): steady-clock completion time of the submission
+    int Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* rem, int64_t* retry, int64_t* reset,
+             int64_t* done_ns = nullptr);
+    rl_coalescer_stats Stats();
+    void Shutdown();
+
+private:
+    void submitter();
+    void completer();
+
+    std::unique_ptr<Backend> be_;
+    rl_coalescer_opts o_;
+    std::vector<Slot> slots_;
+    std::mutex mu_;
+    std::condition_variable cv_sub_, cv_done_, cv_space_;
+    std::deque<Sub*> queue_;                       // submissions with requests not yet launched
+    std::unordered_map<uint64_t, Sub*> subs_;      // by ticket, until waited for
+    std::deque<int> launched_;                     // slots on the device, in launch order
+    uint64_t next_seq_ = 0, pending_ = 0;
+    int inflight_ = 0, next_slot_ = 0;
+    bool stop_ = false, sub_exited_ = false;
+    rl_coalescer_stats st_{};
+    std::thread t_sub_, t_done_;
+};
+
+// the C++ object behind a C-ABI handle (bench_e2e reads completion times)
+Coalescer* unwrap(rl_coalescer* c);
+
+}  // namespace rlc

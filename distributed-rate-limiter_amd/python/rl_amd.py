@@ -72,7 +72,22 @@ class rll_result(C.Structure):
     ]
 
 
+class rl_coalescer_opts(C.Structure):
+    _fields_ = [
+        ("max_batch", C.c_uint32),
+        ("max_in_flight", C.c_uint32),
+        ("linger_ns", C.c_int64),
+        ("queue_cap", C.c_uint64),
+    ]
+
+
+class rl_coalescer_stats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("submitted", "decided", "batches", "max_batch_seen", "pending")]
+
+
 vp = C.c_void_p
+# rl_batch_fn (include/rl_coalescer.h)
+BATCH_FN = C.CFUNCTYPE(C.c_int, vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp)
 _sig = {
     "rl_engine_create": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp)]),
     "rl_engine_destroy": (C.c_int, [vp]),
@@ -103,6 +118,13 @@ _sig = {
     "rll_reset": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int64, C.c_char_p, C.c_size_t]),
     "rll_close": (C.c_int, [vp]),
     "rll_free": (C.c_int, [vp]),
+    "rl_coalescer_create": (C.c_int, [vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
+    "rl_coalescer_create_with_backend": (C.c_int, [BATCH_FN, vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
+    "rl_coalescer_destroy": (C.c_int, [vp]),
+    "rl_coalescer_submit": (C.c_int, [vp, C.c_size_t, vp, vp, vp, vp, C.POINTER(C.c_uint64)]),
+    "rl_coalescer_wait": (C.c_int, [vp, C.c_uint64, C.c_int64, vp, vp, vp, vp]),
+    "rl_coalescer_decide": (C.c_int, [vp, C.c_uint64, C.c_int64, C.c_int64, C.c_uint32, vp, vp, vp, vp]),
+    "rl_coalescer_get_stats": (C.c_int, [vp, C.POINTER(rl_coalescer_stats)]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -361,3 +383,64 @@ def new_limiter(engine: LimiterEngine | None, algorithm, limit, window_ns, prefi
     if rc != RLL_OK:
         raise GoError(rc, buf.value.decode())
     return RateLimiter(h)
+
+
+RL_EAGAIN, RL_ECLOSED = -11, -32
+
+
+class Coalescer:
+    """rl_coalescer (include/rl_coalescer.h): concurrent submissions gathered
+    into engine batches.  `engine` is an Engine (GPU) or, for the CPU tests of
+    the batching logic, a Python function with rl_decide_batch's host-array
+    signature (the test seam rl_coalescer_create_with_backend)."""
+
+    def __init__(self, engine, max_batch=65536, max_in_flight=3, linger_ns=0, queue_cap=0):
+        o = rl_coalescer_opts(max_batch, max_in_flight, linger_ns, queue_cap)
+        h = vp()
+        if isinstance(engine, Engine):
+            rc = lib.rl_coalescer_create(engine.h, C.byref(o), C.byref(h))
+            self._fn = None
+        else:
+            self._fn = BATCH_FN(engine)   # kept alive with the coalescer
+            rc = lib.rl_coalescer_create_with_backend(self._fn, None, C.byref(o), C.byref(h))
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_coalescer_create failed")
+        self.h = h
+
+    def submit(self, key, ts, n, cfg) -> int:
+        key = np.ascontiguousarray(key, dtype=np.uint64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        n = np.ascontiguousarray(n, dtype=np.int64)
+        cfg = np.ascontiguousarray(cfg, dtype=np.uint32)
+        t = C.c_uint64()
+        rc = lib.rl_coalescer_submit(self.h, key.size, _ptr(key), _ptr(ts), _ptr(n), _ptr(cfg), C.byref(t))
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_coalescer_submit failed")
+        return t.value
+
+    def wait(self, ticket: int, m: int, timeout_ns=-1):
+        out = (np.empty(m, np.uint8), np.empty(m, np.int64), np.empty(m, np.int64), np.empty(m, np.int64))
+        rc = lib.rl_coalescer_wait(self.h, ticket, timeout_ns, *[_ptr(x) for x in out])
+        return rc, out
+
+    def decide(self, key, ts, n, cfg):
+        d, rem, retry, reset = C.c_uint8(), C.c_int64(), C.c_int64(), C.c_int64()
+        rc = lib.rl_coalescer_decide(self.h, key, ts, n, cfg, C.byref(d), C.byref(rem), C.byref(retry),
+                                     C.byref(reset))
+        return rc, (d.value, rem.value, retry.value, reset.value)
+
+    def stats(self) -> rl_coalescer_stats:
+        st = rl_coalescer_stats()
+        lib.rl_coalescer_get_stats(self.h, C.byref(st))
+        return st
+
+    def close(self):
+        if self.h:
+            lib.rl_coalescer_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -64,4 +64,5 @@ for r in stats:
         traffic[k] = {"bytes_per_launch": 2 * sum(f) / len(f) * 1024 + sum(w) / len(w) * 1024,
                       "fetch_x2_bytes": 2 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024,
                       "avg_ns": float(r["AverageNs"])}
-json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+if traffic:   # a trace-only run (NO_PMC) keeps the last PMC passes' numbers
+    json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)

@@ -9,6 +9,15 @@ import sys
 
 import pytest
 
+# torch bundles its own libamdhip64.so; the engine library links the system
+# one under the same soname.  Whichever loads first serves both, and torch
+# only initializes with its own: load torch before anything loads the engine
+# (bench.py imports torch first for the same reason).
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "distributed-rate-limiter_amd")
 for p in (ROOT, os.path.join(PKG, "python")):

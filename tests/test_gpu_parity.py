@@ -88,6 +88,33 @@ def test_random_traces(rl, profile, kind, ff):
     run_both(rl, profile, configs, split(tr, [1, 7, 1000, 9000, 20000, 29992]))
 
 
+@pytest.mark.parametrize("small", [True, False])
+@pytest.mark.parametrize("kind", ["tb", "mixed"])
+def test_small_batches(rl, kind, small, monkeypatch):
+    """Batches at and around the single-workgroup path's limit (k_small, 4096),
+    with that path on and off (RL_SMALL_MAX=0: the full launch sequence)."""
+    monkeypatch.setenv("RL_SMALL_MAX", "4096" if small else "0")
+    configs = CONFIG_SETS[kind]
+    tr = random_trace(90 + len(kind), 30_000, 150, configs, big_n=True)
+    sizes = [1, 2, 3, 63, 64, 65, 1000, 4095, 4096, 4097, 129, 2048, 7000]
+    sizes.append(30_000 - sum(sizes))
+    for profile in (0, 1):
+        run_both(rl, profile, configs, split(tr, sizes))
+
+
+@pytest.mark.parametrize("small", [True, False])
+def test_small_batch_single_hot_key(rl, small, monkeypatch):
+    monkeypatch.setenv("RL_SMALL_MAX", "4096" if small else "0")
+    configs = [(1, 20, 12 * NS), (2, 100, 60 * NS), (3, 100, 60 * NS)]
+    rng = np.random.default_rng(8)
+    for c in range(3):
+        m = 4096 * 3
+        key = np.full(m, 5 + c, np.uint64)
+        ts = T0 + np.cumsum(rng.integers(0, 3_000_000, m)).astype(np.int64)
+        cfg = np.full(m, c, np.uint32)
+        run_both(rl, 0, configs, split((key, ts, np.ones(m, np.int64), cfg, None), [4096, 4096, 4096]))
+
+
 def test_hot_keys_long_segments(rl):
     # a few keys carrying most traffic: long per-key segments in one batch
     configs = CONFIG_SETS["mixed"]
