@@ -53,10 +53,10 @@ constexpr int64_t BIN_LO = 1LL << 52, BIN_HI = 1LL << 53;
 constexpr uint32_t NO_STOP = 0xffffffffu;
 
 #ifndef RL_CH_NP
-#define RL_CH_NP 6
+#define RL_CH_NP 7
 #endif
 #ifndef RL_CH_K
-#define RL_CH_K 4
+#define RL_CH_K 5
 #endif
 constexpr int CH_K = RL_CH_K;                          // requests per producer lane
 constexpr int CH_NP = RL_CH_NP;                        // producer waves
@@ -84,7 +84,10 @@ constexpr double CH_YSCALE = 1.0 - 0x1p-28;
 // cycle (lane l reads granule G0 + 4l + j) hit distinct banks, while a row of
 // 16 slots still holds 16 consecutive granules (the loader's LDS-DMA writes
 // slots lane-linearly and swizzles the SOURCE address instead).
-constexpr uint32_t RING = 8192;                  // positions
+#ifndef RL_RING
+#define RL_RING 8192
+#endif
+constexpr uint32_t RING = RL_RING;               // positions
 constexpr uint32_t RING_G = RING / 2;            // granules
 __host__ __device__ constexpr uint32_t swz(uint32_t g) { return (g & ~15u) | ((g & 15u) ^ ((g >> 4) & 3u)); }
 __host__ __device__ constexpr uint32_t ring_slot(uint32_t granule) { return swz(granule & (RING_G - 1)); }

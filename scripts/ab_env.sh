@@ -1,2 +1,10 @@
-for pg in 4096 1024 512 256; do RL_PROBE_GRID=$pg TAG=probe$pg bash scripts/bench_brief.sh | head -1; done
-for pg in 4096 1024 512; do RL_PERM_GRID=$pg TAG=perm$pg bash scripts/bench_brief.sh | head -1; done
+#!/bin/bash
+# A/B of engine environment knobs: each argument is an env assignment list
+# ("-" = none); runs alternate, twice; prints value and per-stage ms.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+for rep in 1 2; do
+  for v in "$@"; do
+    env $( [ "$v" != "-" ] && echo $v ) timeout -k 10 200 python bench.py --steps ${STEPS:-20} --warmup 3 --lat-batches 0 --no-cpu-baseline ${BARGS:-} \
+      | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', round(d['value']/1e6,1), {k: round(x,4) for k,x in d['stages_ms_per_batch'].items()})" || exit 1
+  done
+done
