@@ -901,6 +901,78 @@ extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t 
     return RL_OK;
 }
 
+extern "C" int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* out) {
+    if (!e || !out) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    unsigned long long* d = nullptr;
+    HIPCHK(e, hipMalloc(&d, 4 * sizeof(unsigned long long)));
+    unsigned long long h[4] = {0, 0, 0, 0};
+    hipStream_t s = e->stream;
+    bool ok = hipMemsetAsync(d, 0, sizeof h, s) == hipSuccess;
+    k_table_count<<<1024, 256, 0, s>>>(e->d_tb, e->tb_cap, now_ms, e->profile, d);
+    k_table_count<<<1024, 256, 0, s>>>(e->d_win, e->win_cap, now_ms, e->profile, d + 2);
+    ok = ok && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess;
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok) return fail(e, RL_EDEVICE, "table count failed");
+    *out = rl_table_info{e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3]};
+    return RL_OK;
+}
+
+extern "C" int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, uint64_t win_capacity,
+                           rl_table_info* out) {
+    if (!e) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    const uint64_t tb_cap = tb_capacity ? pow2_at_least(std::max<uint64_t>(tb_capacity, 1024)) : e->tb_cap;
+    const uint64_t win_cap = win_capacity ? pow2_at_least(std::max<uint64_t>(win_capacity, 1024)) : e->win_cap;
+    if (tb_cap + win_cap >= (1ull << 31)) return fail(e, RL_EINVAL, "table capacities too large");
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    TbEntry* ntb = nullptr;
+    WinEntry* nwin = nullptr;
+    unsigned long long* d = nullptr;
+    bool ok = hipMalloc(&ntb, sizeof(TbEntry) * tb_cap) == hipSuccess;
+    ok = ok && hipMalloc(&nwin, sizeof(WinEntry) * win_cap) == hipSuccess;
+    ok = ok && hipMalloc(&d, 4 * sizeof(unsigned long long)) == hipSuccess;
+    if (!ok) {
+        (void)hipFree(ntb); (void)hipFree(nwin); (void)hipFree(d);
+        return fail(e, RL_ENOMEM, "table gc: allocation failed");
+    }
+    unsigned long long h[4] = {0, 0, 0, 0};
+    hipStream_t s = e->stream;
+    k_init_tb<<<2048, 256, 0, s>>>(ntb, tb_cap);
+    k_init_win<<<2048, 256, 0, s>>>(nwin, win_cap);
+    ok = hipMemsetAsync(d, 0, sizeof h, s) == hipSuccess;
+    k_rehash<<<2048, 256, 0, s>>>(e->d_tb, e->tb_cap, ntb, tb_cap - 1, now_ms, e->profile, d);
+    k_rehash<<<2048, 256, 0, s>>>(e->d_win, e->win_cap, nwin, win_cap - 1, now_ms, e->profile, d + 2);
+    ok = ok && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess;
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    (void)hipFree(d);
+    if (!ok || h[1] || h[3]) {
+        (void)hipFree(ntb);
+        (void)hipFree(nwin);
+        return ok ? fail(e, RL_ENOMEM, "table gc: live keys do not fit the requested capacity")
+                  : fail(e, RL_EDEVICE, "table gc failed");
+    }
+    (void)hipFree(e->d_tb);
+    (void)hipFree(e->d_win);
+    e->d_tb = ntb;
+    e->d_win = nwin;
+    // slot ids (the sort keys) follow the capacities
+    e->tb_cap = tb_cap;
+    e->win_cap = win_cap;
+    e->win_base = (uint32_t)tb_cap;
+    e->invalid_key = (uint32_t)(tb_cap + win_cap);
+    e->sort_bits = bitlen(e->invalid_key);
+    e->sort_passes = (e->sort_bits + 7) / 8;
+    e->stats.sort_bits = e->sort_bits;
+    e->stats.sort_passes = e->sort_passes;
+    if (out) *out = rl_table_info{tb_cap, h[0], h[0], win_cap, h[2], h[2]};
+    return RL_OK;
+}
+
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     if (!e || !out) return RL_EINVAL;
     (void)hipSetDevice(e->device);

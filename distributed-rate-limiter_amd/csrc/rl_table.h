@@ -76,4 +76,52 @@ __device__ inline uint32_t probe_find(const E* tab, uint64_t mask, uint64_t k) {
     return NO_SLOT;
 }
 
+// Liveness at server clock now_ms, as Redis's expiry sees it: a token-bucket
+// entry is its hash key; a window entry holds up to two counter keys and lives
+// while either does (lazy expiry would treat the others as absent anyway).
+__device__ inline bool entry_live(const TbEntry& x, int64_t now_ms, int32_t profile) {
+    return x.key != EMPTY_KEY && x.when != ABSENT && key_alive(x.when, now_ms, profile);
+}
+__device__ inline bool entry_live(const WinEntry& x, int64_t now_ms, int32_t profile) {
+    if (x.key == EMPTY_KEY) return false;
+    for (int k = 0; k < 2; k++)
+        if (x.s[k].when != ABSENT && key_alive(x.s[k].when, now_ms, profile)) return true;
+    return false;
+}
+
+// Table GC / resize (rl_table_gc): re-insert every live entry of `old` into
+// the empty table `nu`.  Keys are distinct, so concurrent inserts never race
+// on one key.  counters[0] += live entries, counters[1] += entries that found
+// no slot (the new table is too small: the caller keeps the old one).
+template <typename E>
+__global__ void k_rehash(const E* __restrict__ old, uint64_t n_old, E* nu, uint64_t mask_new, int64_t now_ms,
+                         int32_t profile, unsigned long long* counters) {
+    unsigned long long live = 0, lost = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_old;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const E x = old[i];
+        if (!entry_live(x, now_ms, profile)) continue;
+        live++;
+        const uint32_t s = probe_insert(nu, mask_new, x.key);
+        if (s == NO_SLOT) { lost++; continue; }
+        nu[s] = x;
+    }
+    if (live) atomicAdd(&counters[0], live);
+    if (lost) atomicAdd(&counters[1], lost);
+}
+
+// occupied and live entries (rl_table_info_get)
+template <typename E>
+__global__ void k_table_count(const E* __restrict__ t, uint64_t n, int64_t now_ms, int32_t profile,
+                              unsigned long long* counters) {
+    unsigned long long used = 0, live = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const E x = t[i];
+        used += x.key != EMPTY_KEY;
+        live += entry_live(x, now_ms, profile);
+    }
+    if (used) atomicAdd(&counters[0], used);
+    if (live) atomicAdd(&counters[1], live);
+}
+
 }  // namespace rl

@@ -72,6 +72,11 @@ class rll_result(C.Structure):
     ]
 
 
+class rl_table_info(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("tb_capacity", "tb_used", "tb_live", "win_capacity", "win_used",
+                                          "win_live")]
+
+
 class rl_coalescer_opts(C.Structure):
     _fields_ = [
         ("max_batch", C.c_uint32),
@@ -98,6 +103,8 @@ _sig = {
     "rl_reset": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_int64]),
     "rl_engine_stats": (C.c_int, [vp, C.POINTER(rl_stats)]),
     "rl_engine_set_timing": (C.c_int, [vp, C.c_int]),
+    "rl_table_info_get": (C.c_int, [vp, C.c_int64, C.POINTER(rl_table_info)]),
+    "rl_table_gc": (C.c_int, [vp, C.c_int64, C.c_uint64, C.c_uint64, C.POINTER(rl_table_info)]),
     "rl_engine_stage_times": (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_uint64)]),
     "rl_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
     "rl_engine_debug_words": (C.c_int, [vp, vp, C.c_size_t]),
@@ -239,6 +246,20 @@ class Engine:
         out = np.zeros(n, np.uint32)
         lib.rl_engine_debug_words(self.h, _ptr(out), n)
         return out
+
+    def table_info(self, now_ms: int) -> rl_table_info:
+        out = rl_table_info()
+        rc = lib.rl_table_info_get(self.h, now_ms, C.byref(out))
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+        return out
+
+    def table_gc(self, now_ms: int, tb_capacity=0, win_capacity=0, check=True):
+        out = rl_table_info()
+        rc = lib.rl_table_gc(self.h, now_ms, tb_capacity, win_capacity, C.byref(out))
+        if check and rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+        return rc, out
 
     def set_timing(self, on: bool):
         lib.rl_engine_set_timing(self.h, 1 if on else 0)

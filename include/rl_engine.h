@@ -132,6 +132,25 @@ int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns);
 
 int rl_engine_stats(rl_engine* e, rl_stats* out);
 
+/* State-table occupancy.  A key is live at server clock now_ms when its Redis
+ * TTL has not expired (a window entry: either of its two counter keys). */
+typedef struct rl_table_info {
+    uint64_t tb_capacity, tb_used, tb_live;
+    uint64_t win_capacity, win_used, win_live;
+} rl_table_info;
+int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* out);
+
+/* Table GC (the TTLs of tokenbucket.go:170,
+ * slidingwindow.go:161-162, fixedwindow.go:151): drop every key expired at
+ * server clock now_ms -- Redis's active expiry -- and optionally resize the
+ * tables (0 = keep the capacity).  Keys are only ever inserted by the decision
+ * path, so this is what keeps a long-running table from filling.  Decisions
+ * are unchanged provided no later request carries a server clock below
+ * now_ms (lazy expiry would see those keys as absent anyway).  Synchronous;
+ * waits for queued batches.  RL_ENOMEM (old tables kept) when the live keys do
+ * not fit the requested capacity.  `out` (nullable): the tables afterwards. */
+int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, uint64_t win_capacity, rl_table_info* out);
+
 /* per-stage device time (ms) accumulated since the last call, measured with
  * HIP events on the stream the kernels run on; stages: 0 probe, 1 sort,
  * 2 segments + permute, 3 replay (k_tb_chain), 4 finish (run expansion +

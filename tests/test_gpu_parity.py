@@ -289,3 +289,80 @@ def test_device_api_batches_in_flight(rl, pipeline):
         ref = sim.decide(key, ts, n, cfg)
         res = rl.Decisions(*[x.cpu().numpy() for x in o])
         assert_same(res, ref, configs, cfg, what=f"batch {i}")
+
+
+# --- table GC / resize (rl_table_gc) ----------------------------------------------
+
+@pytest.mark.parametrize("profile", [0, 1])
+def test_table_gc_keeps_decisions(rl, profile):
+    """GC at the clock of the next batch (then grow, then shrink) between
+    batches: decisions stay identical to the oracle, which never collects."""
+    configs = CONFIG_SETS["mixed"]
+    tr = random_trace(200 + profile, 60_000, 3000, configs, big_n=True)
+    eng = make_engine(rl, profile, tb=1 << 14, win=1 << 14, max_batch=1 << 15)
+    sim = oracle.OracleSim(profile)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    parts = split(tr, [15_000, 15_000, 15_000, 15_000])
+    caps = [(0, 0), (1 << 16, 1 << 15), (1 << 13, 1 << 13)]
+    for i, (key, ts, n, cfg, sms) in enumerate(parts):
+        if i:
+            now_ms = int(ts[0]) // 1_000_000
+            before = eng.table_info(now_ms)
+            _, after = eng.table_gc(now_ms, *caps[i - 1])
+            assert after.tb_live == before.tb_live and after.win_live == before.win_live
+            assert after.tb_used == after.tb_live <= before.tb_used
+            if caps[i - 1][0]:
+                assert after.tb_capacity == caps[i - 1][0] and after.win_capacity == caps[i - 1][1]
+        res = eng.decide(key, ts, n, cfg, sms)
+        assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
+
+
+def test_table_gc_frees_a_full_table(rl):
+    """A table that is full of expired keys accepts new keys after GC; a GC
+    whose live keys do not fit the requested size fails and keeps the tables."""
+    configs = [(1, 5, NS), (3, 5, NS)]   # TB ttl 2 s, FW ttl 1 s
+    eng = make_engine(rl, 0, tb=1024, win=1024, max_batch=4096)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    m = 2000
+    for rnd in range(3):
+        key = (np.arange(m, dtype=np.uint64) + rnd * m)
+        ts = np.full(m, T0 + rnd * 10 * NS, np.int64)
+        n = np.ones(m, np.int64)
+        cfg = (key % 2).astype(np.uint32)
+        if rnd:
+            info = eng.table_info(int(ts[0]) // 1_000_000)
+            assert info.tb_used == 1000 and info.tb_live == 0 and info.win_live == 0
+            eng.table_gc(int(ts[0]) // 1_000_000)
+            info = eng.table_info(int(ts[0]) // 1_000_000)
+            assert info.tb_used == 0 and info.win_used == 0
+        res = eng.decide(key, ts, n, cfg)
+        assert_same(res, sim.decide(key, ts, n, cfg), configs, cfg, what=f"round {rnd}")
+    eng.close()
+
+
+def test_table_gc_refuses_a_too_small_table(rl):
+    configs = [(1, 5, 60 * NS)]
+    eng = make_engine(rl, 0, tb=4096, win=1024, max_batch=4096)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    m = 3000
+    key = np.arange(m, dtype=np.uint64)
+    n = np.ones(m, np.int64)
+    cfg = np.zeros(m, np.uint32)
+    for rnd in range(2):
+        ts = np.full(m, T0 + rnd * NS, np.int64)
+        if rnd:
+            rc, _ = eng.table_gc(int(ts[0]) // 1_000_000, 1024, 1024, check=False)
+            assert rc == rl.RL_ENOMEM
+            info = eng.table_info(int(ts[0]) // 1_000_000)
+            assert info.tb_capacity == 4096 and info.tb_live == m
+        res = eng.decide(key, ts, n, cfg)
+        assert_same(res, sim.decide(key, ts, n, cfg), configs, cfg, what=f"round {rnd}")
+    eng.close()
