@@ -234,8 +234,11 @@ int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const in
             s->done_ns = steady_ns();
         }
         *ticket = s->first;
+        // wake the submitter only when it sleeps: at millions of submissions
+        // per second an unconditional notify is a futex call per submission
+        if (!m || !sub_idle_) return RL_OK;
     }
-    if (m) cv_sub_.notify_one();
+    cv_sub_.notify_one();
     return RL_OK;
 }
 
@@ -245,10 +248,14 @@ int Coalescer::Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* 
     auto it = subs_.find(ticket);
     if (it == subs_.end()) return RL_EINVAL;
     Sub* s = it->second;
-    if (timeout_ns < 0) {
-        s->cv.wait(lk, [&] { return s->done; });
-    } else if (!s->cv.wait_for(lk, std::chrono::nanoseconds(timeout_ns), [&] { return s->done; })) {
-        return RL_ETIMEOUT;
+    if (!s->done) {
+        s->waiting = true;
+        if (timeout_ns < 0) {
+            s->cv.wait(lk, [&] { return s->done; });
+        } else if (!s->cv.wait_for(lk, std::chrono::nanoseconds(timeout_ns), [&] { return s->done; })) {
+            s->waiting = false;
+            return RL_ETIMEOUT;
+        }
     }
     subs_.erase(it);
     lk.unlock();
@@ -273,11 +280,15 @@ rl_coalescer_stats Coalescer::Stats() {
 void Coalescer::submitter() {
     for (;;) {
         std::unique_lock<std::mutex> lk(mu_);
+        sub_idle_ = true;
         cv_sub_.wait(lk, [&] { return (stop_ && pending_ == 0) || (pending_ > 0 && inflight_ < (int)o_.max_in_flight); });
+        sub_idle_ = false;
         if (pending_ == 0) break;   // stop_ with nothing left
         if (o_.linger_ns > 0 && inflight_ == 0 && pending_ < o_.max_batch && !stop_) {
             const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(o_.linger_ns);
+            sub_idle_ = true;
             cv_sub_.wait_until(lk, until, [&] { return stop_ || pending_ >= o_.max_batch; });
+            sub_idle_ = false;
         }
         const int si = next_slot_;
         next_slot_ = (next_slot_ + 1) % (int)o_.max_in_flight;
@@ -334,8 +345,10 @@ void Coalescer::completer() {
             memcpy(p.sub->reset + p.off, s.reset + p.at, 8 * p.count);
         }
         const int64_t now = steady_ns();
+        bool wake;
         {
             std::lock_guard<std::mutex> g(mu_);
+            wake = sub_idle_;
             launched_.pop_front();
             inflight_--;
             st_.decided += s.m;
@@ -346,11 +359,11 @@ void Coalescer::completer() {
                 if (sub->left == 0) {
                     sub->done = true;
                     sub->done_ns = now;
-                    sub->cv.notify_all();
+                    if (sub->waiting) sub->cv.notify_all();
                 }
             }
         }
-        cv_sub_.notify_one();
+        if (wake) cv_sub_.notify_one();
     }
 }
 

@@ -60,6 +60,7 @@ struct Sub {
     size_t m = 0, taken = 0, left = 0;
     int status = RL_OK;
     bool done = false;
+    bool waiting = false;         // a caller blocks on cv (else completion skips the wake)
     int64_t done_ns = 0;          // steady clock at completion
     std::condition_variable cv;
     std::unique_ptr<uint8_t[]> mem;
@@ -100,6 +101,7 @@ private:
     uint64_t next_seq_ = 0, pending_ = 0;
     int inflight_ = 0, next_slot_ = 0;
     bool stop_ = false, sub_exited_ = false;
+    bool sub_idle_ = false;        // the submitter sleeps on cv_sub_ (submit wakes it only then)
     rl_coalescer_stats st_{};
     std::thread t_sub_, t_done_;
 };
