@@ -73,7 +73,10 @@ __device__ inline int ch_producer_index(uint32_t wave) {
     return wave == 0 || wave == (uint32_t)CH_LOADER ? -1 : (int)wave - (wave < (uint32_t)CH_LOADER ? 1 : 2);
 }
 constexpr int CH_BLOCK = (CH_NP + 2) * 64;
-constexpr int CH_SERIAL = 64;                          // serial exact steps per round at most
+#ifndef RL_CH_SERIAL
+#define RL_CH_SERIAL 64
+#endif
+constexpr int CH_SERIAL = RL_CH_SERIAL;                // serial exact steps per round at most
 // conservative scale of the allow/clamp threshold th*P (covers the rounding of
 // th*P and of the bound arithmetic with a wide margin)
 constexpr double CH_YSCALE = 1.0 - 0x1p-28;
@@ -683,16 +686,25 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     int32_t mode = fast_mode(D, E, profile);
     double Ps = 1.0, Rs = 1.0;
     if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
-    const uint32_t pq = q + lane;                   // n and cfg of the next 64 positions, one load
-    const int64_t nvec = pq < j1 ? a.n[pq] : 1;
-    const uint32_t cvec = pq < j1 ? a.cfg[pq] : 0u;
+    // every input of the next 64 positions in one vector load each (lane k holds
+    // position q + k): the steps below read registers only, so a step costs its
+    // arithmetic, not a dependent memory round trip
+    int64_t nvec = 0;
+    double avec = 0.0, capvec = 0.0;
     uint32_t k = 0;
     for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
-        const double add = add_at(q);
+        if ((k & 63u) == 0) {
+            const uint32_t pq = q + lane;
+            nvec = pq < j1 ? a.n[pq] : 1;
+            avec = pq < lim ? add_at(pq) : 0.0;
+            capvec = cfgs[pq < j1 ? a.cfg[pq] : 0u].limit_d;
+        }
+        const uint32_t kl = k & 63u;
+        const double add = __longlong_as_double(readlane_i64(__double_as_longlong(avec), kl));
         const bool alive = add == add;
-        const int64_t nn = readlane_i64(nvec, k);
-        const CfgDev& C = cfgs[(uint32_t)__builtin_amdgcn_readlane((int)cvec, (int)k)];
-        const TbEval v = tb_eval(mode, D, E, Ps, Rs, alive, alive ? add : 0.0, C.limit_d, (double)nn, profile);
+        const int64_t nn = readlane_i64(nvec, kl);
+        const double cap = __longlong_as_double(readlane_i64(__double_as_longlong(capvec), kl));
+        const TbEval v = tb_eval(mode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
         if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
         force = v.allowed || v.clamped || !alive;
         if (mode != QM_NONE && v.inrange) {

@@ -80,6 +80,8 @@ struct Args {
     int gens = 4;
     int device = 0;
     int64_t linger_ns = 0;
+    int64_t limit = 20;          // Token Bucket 100/min burst 20 = {Limit 20, Window 12 s}
+    double window_s = 12.0;
 };
 
 }  // namespace
@@ -104,6 +106,8 @@ int main(int argc, char** argv) {
         else if (k == "--gens") a.gens = atoi(v.c_str());
         else if (k == "--device") a.device = atoi(v.c_str());
         else if (k == "--linger-us") a.linger_ns = (int64_t)(atof(v.c_str()) * 1000);
+        else if (k == "--limit") a.limit = atol(v.c_str());
+        else if (k == "--window-s") a.window_s = atof(v.c_str());
         else { fprintf(stderr, "unknown option %s\n", k.c_str()); return 2; }
     }
 
@@ -131,7 +135,7 @@ int main(int argc, char** argv) {
     rl_engine* e = nullptr;
     if (rl_engine_create(&o, &e) != RL_OK) { fprintf(stderr, "engine create failed\n"); return 1; }
     uint32_t cfg = 0;
-    if (rl_config_register(e, RL_ALG_TOKEN_BUCKET, 20, 12 * NS, &cfg) != RL_OK) return 1;
+    if (rl_config_register(e, RL_ALG_TOKEN_BUCKET, a.limit, (int64_t)(a.window_s * NS), &cfg) != RL_OK) return 1;
     rl_coalescer_opts co{};
     co.max_batch = a.max_batch;
     co.max_in_flight = 3;
