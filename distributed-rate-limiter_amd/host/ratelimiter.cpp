@@ -337,6 +337,16 @@ Error construct(Engine* engine, const Config* config, std::unique_ptr<RateLimite
 
 // As in the reference, the constructor (not Config.Algorithm) selects the
 // algorithm; Config.Algorithm must still pass Validate (tokenbucket.go:71-75).
+// result.go:5-50
+Result NewAllowedResult(int64_t limit, int64_t remaining, int64_t reset_at) {
+    return Result{true, limit, remaining, 0, reset_at};
+}
+Result NewDeniedResult(int64_t limit, int64_t retry_after, int64_t reset_at) {
+    return Result{false, limit, 0, retry_after, reset_at};
+}
+Result NewFailOpenResult() { return Result{true, 0, 0, 0, ZeroTime}; }
+Result NewFailClosedResult() { return Result{false, 0, 0, 0, ZeroTime}; }
+
 Error NewTokenBucket(Engine* e, const Config* c, std::unique_ptr<RateLimiter>* out) {
     return construct(e, c, out, rl::ALG_TOKEN_BUCKET);
 }
@@ -450,6 +460,30 @@ static void to_c(const Result& r, rll_result* o) {
     o->remaining = r.Remaining;
     o->retry_after_ns = r.RetryAfter;
     o->reset_at_ns = r.ResetAt;
+}
+
+extern "C" int rll_new_allowed_result(int64_t limit, int64_t remaining, int64_t reset_at_ns, rll_result* out) {
+    if (!out) return RLL_ERR_ARG;
+    to_c(NewAllowedResult(limit, remaining, reset_at_ns), out);
+    return RLL_OK;
+}
+
+extern "C" int rll_new_denied_result(int64_t limit, int64_t retry_after_ns, int64_t reset_at_ns, rll_result* out) {
+    if (!out) return RLL_ERR_ARG;
+    to_c(NewDeniedResult(limit, retry_after_ns, reset_at_ns), out);
+    return RLL_OK;
+}
+
+extern "C" int rll_new_fail_open_result(rll_result* out) {
+    if (!out) return RLL_ERR_ARG;
+    to_c(NewFailOpenResult(), out);
+    return RLL_OK;
+}
+
+extern "C" int rll_new_fail_closed_result(rll_result* out) {
+    if (!out) return RLL_ERR_ARG;
+    to_c(NewFailClosedResult(), out);
+    return RLL_OK;
 }
 
 static int code_of(const Error& e) {

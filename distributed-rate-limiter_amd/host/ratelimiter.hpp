@@ -61,6 +61,15 @@ struct Result {
     int64_t ResetAt = 0;     // time.Time as Unix ns
 };
 
+// time.Time{} (the zero Time) as a ResetAt value
+constexpr int64_t ZeroTime = INT64_MIN;
+
+// Result constructors (result.go:5-50)
+Result NewAllowedResult(int64_t limit, int64_t remaining, int64_t reset_at);
+Result NewDeniedResult(int64_t limit, int64_t retry_after, int64_t reset_at);
+Result NewFailOpenResult();
+Result NewFailClosedResult();
+
 struct Config {
     Algorithm algorithm;
     int64_t Limit = 0;

@@ -125,6 +125,10 @@ _sig = {
     "rll_reset": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.c_int64, C.c_char_p, C.c_size_t]),
     "rll_close": (C.c_int, [vp]),
     "rll_free": (C.c_int, [vp]),
+    "rll_new_allowed_result": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.POINTER(rll_result)]),
+    "rll_new_denied_result": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.POINTER(rll_result)]),
+    "rll_new_fail_open_result": (C.c_int, [C.POINTER(rll_result)]),
+    "rll_new_fail_closed_result": (C.c_int, [C.POINTER(rll_result)]),
     "rl_coalescer_create": (C.c_int, [vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_create_with_backend": (C.c_int, [BATCH_FN, vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_destroy": (C.c_int, [vp]),

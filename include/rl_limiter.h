@@ -42,6 +42,15 @@ typedef struct rll_result {
     int64_t reset_at_ns;
 } rll_result;
 
+#define RLL_TIME_ZERO INT64_MIN   /* reset_at_ns of time.Time{} */
+
+/* Result constructors (result.go:5-50): NewAllowedResult, NewDeniedResult,
+ * NewFailOpenResult, NewFailClosedResult */
+int rll_new_allowed_result(int64_t limit, int64_t remaining, int64_t reset_at_ns, rll_result* out);
+int rll_new_denied_result(int64_t limit, int64_t retry_after_ns, int64_t reset_at_ns, rll_result* out);
+int rll_new_fail_open_result(rll_result* out);
+int rll_new_fail_closed_result(rll_result* out);
+
 int rll_engine_new(const rl_opts* opts, rll_engine** out, char* err, size_t errlen);
 int rll_engine_free(rll_engine* e);
 rl_engine* rll_engine_raw(rll_engine* e);
