@@ -1,6 +1,7 @@
 // ratelimiter.cpp -- host mirror of the reference's Go `internal/ratelimiter`
 // package over the MI355X engine.  See ratelimiter.hpp for the mapping.
 #include "ratelimiter.hpp"
+#include "decorators.hpp"
 
 #include <time.h>
 
@@ -370,6 +371,7 @@ struct rll_engine {
 };
 struct rll_limiter {
     std::unique_ptr<RateLimiter> lim;
+    MetricsDecorator* metrics = nullptr;   // inside lim, when rll_add_metrics wrapped it
 };
 
 static void put_err(char* err, size_t len, const std::string& s) {
@@ -460,6 +462,33 @@ static void to_c(const Result& r, rll_result* o) {
     o->remaining = r.Remaining;
     o->retry_after_ns = r.RetryAfter;
     o->reset_at_ns = r.ResetAt;
+}
+
+extern "C" int rll_add_metrics(rll_limiter* l) {
+    if (!l || !l->lim || l->metrics) return RLL_ERR_ARG;
+    auto* m = new MetricsDecorator(std::move(l->lim));
+    l->lim.reset(m);
+    l->metrics = m;
+    return RLL_OK;
+}
+
+extern "C" int rll_metrics_expose(rll_limiter* l, char* buf, size_t len) {
+    if (!l || !l->metrics) return -RLL_ERR_ARG;
+    const std::string s = l->metrics->Expose();
+    if (buf && len) snprintf(buf, len, "%s", s.c_str());
+    return (int)s.size();
+}
+
+extern "C" int rll_add_logging(rll_limiter* l, rll_log_fn fn, void* user) {
+    if (!l || !l->lim || !fn) return RLL_ERR_ARG;
+    l->lim.reset(new LoggingDecorator(
+        std::move(l->lim),
+        [fn, user](LogLevel lv, const std::string& msg, const std::vector<std::pair<std::string, std::string>>& f) {
+            std::string kv;
+            for (const auto& p : f) kv += (kv.empty() ? "" : " ") + p.first + "=" + p.second;
+            fn(user, (int)lv, msg.c_str(), kv.c_str());
+        }));
+    return RLL_OK;
 }
 
 extern "C" int rll_new_allowed_result(int64_t limit, int64_t remaining, int64_t reset_at_ns, rll_result* out) {

@@ -93,6 +93,8 @@ class rl_coalescer_stats(C.Structure):
 vp = C.c_void_p
 # rl_batch_fn (include/rl_coalescer.h)
 BATCH_FN = C.CFUNCTYPE(C.c_int, vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp)
+# rll_log_fn (include/rl_limiter.h)
+LOG_FN = C.CFUNCTYPE(None, vp, C.c_int, C.c_char_p, C.c_char_p)
 _sig = {
     "rl_engine_create": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp)]),
     "rl_engine_destroy": (C.c_int, [vp]),
@@ -128,6 +130,9 @@ _sig = {
     "rll_new_allowed_result": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.POINTER(rll_result)]),
     "rll_new_denied_result": (C.c_int, [C.c_int64, C.c_int64, C.c_int64, C.POINTER(rll_result)]),
     "rll_new_fail_open_result": (C.c_int, [C.POINTER(rll_result)]),
+    "rll_add_metrics": (C.c_int, [vp]),
+    "rll_metrics_expose": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
+    "rll_add_logging": (C.c_int, [vp, LOG_FN, vp]),
     "rll_new_fail_closed_result": (C.c_int, [C.POINTER(rll_result)]),
     "rl_coalescer_create": (C.c_int, [vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_create_with_backend": (C.c_int, [BATCH_FN, vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
@@ -381,6 +386,25 @@ class RateLimiter:
                             _ptr(codes))
         res = [Result(bool(o.allowed), o.limit, o.remaining, o.retry_after_ns, o.reset_at_ns) for o in out]
         return res, codes
+
+    def add_metrics(self):
+        """MetricsDecorator (ADR-003) around this limiter, in place."""
+        if lib.rll_add_metrics(self.h) != RLL_OK:
+            raise GoError(RLL_ERR_ARG, "rll_add_metrics failed")
+
+    def metrics_text(self) -> str:
+        n = lib.rll_metrics_expose(self.h, None, 0)
+        if n < 0:
+            raise GoError(RLL_ERR_ARG, "no metrics decorator")
+        buf = C.create_string_buffer(n + 1)
+        lib.rll_metrics_expose(self.h, buf, n + 1)
+        return buf.value.decode()
+
+    def add_logging(self, sink):
+        """LoggingDecorator (ADR-003): sink(level, msg, fields) per record."""
+        self._log_fn = LOG_FN(lambda u, lv, msg, f: sink(lv, msg.decode(), f.decode()))
+        if lib.rll_add_logging(self.h, self._log_fn, None) != RLL_OK:
+            raise GoError(RLL_ERR_ARG, "rll_add_logging failed")
 
     def reset(self, key, now_ns=NOW_WALL):
         buf = C.create_string_buffer(512)

@@ -82,6 +82,17 @@ int rll_allow_n(rll_limiter* l, const char* key, size_t keylen, int64_t n, int64
 int rll_allow_batch(rll_limiter* l, size_t m, const char* const* keys, const size_t* keylens,
                     const int64_t* n, const int64_t* now_ns, rll_result* out, int32_t* codes);
 
+/* Observability decorators (docs/ADR/003-decorator-pattern-for-observability.md):
+ * wrap the limiter in place; every later call goes through them.
+ * rll_metrics_expose writes the Prometheus text exposition
+ * (rate_limiter_requests_total{algorithm,allowed,error},
+ * rate_limiter_decision_seconds histogram) and returns its full length. */
+int rll_add_metrics(rll_limiter* l);
+int rll_metrics_expose(rll_limiter* l, char* buf, size_t len);
+/* level: 0 debug, 1 info, 2 warn, 3 error; fields "k=v k=v" */
+typedef void (*rll_log_fn)(void* user, int level, const char* msg, const char* fields);
+int rll_add_logging(rll_limiter* l, rll_log_fn fn, void* user);
+
 int rll_reset(rll_limiter* l, const char* key, size_t keylen, int64_t now_ns, char* err, size_t errlen);
 int rll_close(rll_limiter* l);   /* Close(): later calls take the storage-error path */
 int rll_free(rll_limiter* l);
