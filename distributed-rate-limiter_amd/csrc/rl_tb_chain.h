@@ -683,9 +683,16 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
                                                                        const CfgDev* __restrict__ cfgs,
                                                                        int32_t profile, const ReqArgs& a) {
     const uint32_t lane = threadIdx.x & 63;
+    // mode: the callers' fast regime (positive digits only).  emode: how a step
+    // is evaluated here -- sign-symmetric, because %.14g / strtod and the
+    // binade scaling are: a negative state in a fast decade (the balance a hot
+    // key random-walks around zero after an allow, its last_refill rounded to
+    // 100 us) steps with the decade arithmetic instead of a full
+    // decimal conversion per step
     int32_t mode = fast_mode(D, E, profile);
+    int32_t emode = fast_mode(D < 0 ? -D : D, E, profile);
     double Ps = 1.0, Rs = 1.0;
-    if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
+    if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
     // every input of the next 64 positions in one vector load each (lane k holds
     // position q + k): the steps below read registers only, so a step costs its
     // arithmetic, not a dependent memory round trip
@@ -704,19 +711,19 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
         const bool alive = add == add;
         const int64_t nn = readlane_i64(nvec, kl);
         const double cap = __longlong_as_double(readlane_i64(__double_as_longlong(capvec), kl));
-        const TbEval v = tb_eval(mode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
+        const TbEval v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
         if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
         force = v.allowed || v.clamped || !alive;
-        if (mode != QM_NONE && v.inrange) {
+        if (emode != QM_NONE && v.inrange) {
             D = v.Dact;                     // same decade / binade (sign may flip)
-            mode = fast_mode(D, E, profile);
         } else {
             const TbQ nq = tb_quant(v.tokens, profile);
             D = nq.D;
             E = nq.E;
-            mode = fast_mode(D, E, profile);
-            if (mode != QM_NONE) mode_scale(mode, E, Ps, Rs);
+            emode = fast_mode(D < 0 ? -D : D, E, profile);
+            if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
         }
+        mode = fast_mode(D, E, profile);
         q++;
     }
     return SerialOut{q, D, E, mode, k};
