@@ -1,0 +1,264 @@
+// On-GPU FormatKey + XXH64 of a batch of raw keys (include/rl_keyhash.h,
+// SURVEY.md §8f rank 3).  Replaces the host string building of
+// config.go:81-87 (FormatKey) and the Redis keyspace's string identity with a
+// 64-bit id per formatted key.
+//
+// Layout: one workgroup hashes KH_BLOCK consecutive keys.  Their bytes are one
+// contiguous range of the input buffer, so the group stages the range into LDS
+// with coalesced 16-byte loads and every lane then reads its key's words from
+// LDS (funnel shift of two aligned 8-byte LDS words), never from HBM with a
+// stride.  A group whose range exceeds the LDS budget (keys averaging more than
+// KH_RAW_BYTES / KH_BLOCK bytes) reads its keys byte by byte from global memory.
+//
+// Traffic per key: len + 8 B offset in, 8 B id out -- an HBM-bound byte kernel,
+// no MFMA.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "../../include/rl_engine.h"
+#include "../../include/rl_keyhash.h"
+
+namespace {
+
+constexpr int KH_BLOCK = 256;                 // keys per workgroup (4 waves)
+constexpr int KH_RAW_BYTES = 24576;           // staged key bytes per workgroup
+constexpr int KH_RAW_WORDS = KH_RAW_BYTES / 8;
+constexpr int KH_PRE_BYTES = 256;             // prefix + ':' (<= 241 bytes used)
+
+// XXH64 constants and rounds (the published XXH64 specification, xxHash 0.8)
+constexpr uint64_t P1 = 0x9E3779B185EBCA87ull;
+constexpr uint64_t P2 = 0xC2B2AE3D27D4EB4Full;
+constexpr uint64_t P3 = 0x165667B19E3779F9ull;
+constexpr uint64_t P4 = 0x85EBCA77C2B2AE63ull;
+constexpr uint64_t P5 = 0x27D4EB2F165667C5ull;
+
+__device__ __forceinline__ uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint64_t xround(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
+__device__ __forceinline__ uint64_t xmerge(uint64_t acc, uint64_t v) { return (acc ^ xround(0, v)) * P1 + P4; }
+
+struct Prefix {
+    uint32_t len1;                 // prefix bytes + 1 for ':' (0: no prefix)
+    uint8_t b[KH_PRE_BYTES];
+};
+
+// Formatted key F = prefix ':' key, read through little-endian words.  The key
+// part comes from LDS (staged) or from global memory (oversized groups).
+template <bool kLds>
+struct Formatted {
+    const uint8_t* pre;            // LDS, 8-byte aligned, zero past plen1, padded by 8
+    uint32_t plen1;
+    const uint64_t* raw;           // LDS words (kLds)
+    uint32_t koff;                 // byte offset of the key in raw (kLds)
+    const uint8_t* g;              // global key start (!kLds)
+
+    __device__ __forceinline__ uint8_t key_byte(uint64_t j) const {
+        if constexpr (kLds) return (uint8_t)(raw[(koff + j) >> 3] >> (((koff + j) & 7) * 8));
+        else return g[j];
+    }
+    __device__ __forceinline__ uint8_t byte(uint64_t i) const {
+        return i < plen1 ? pre[i] : key_byte(i - plen1);
+    }
+    __device__ __forceinline__ uint64_t key_word(uint64_t j) const {
+        if constexpr (kLds) {
+            uint64_t o = koff + j;
+            uint64_t a = raw[o >> 3], b = raw[(o >> 3) + 1];
+            uint32_t sh = (uint32_t)(o & 7) * 8;
+            return sh ? (a >> sh) | (b << (64 - sh)) : a;
+        } else {
+            uint64_t w = 0;
+            for (int k = 0; k < 8; ++k) w |= (uint64_t)g[j + k] << (8 * k);
+            return w;
+        }
+    }
+    // prefix bytes from i on; the LDS copy is zero past plen1, so a word that
+    // straddles into the key has zeros in its key bytes
+    __device__ __forceinline__ uint64_t pre_word(uint64_t i) const {
+        const uint64_t* p64 = reinterpret_cast<const uint64_t*>(pre);
+        uint64_t a = p64[i >> 3], b = p64[(i >> 3) + 1];
+        uint32_t sh = (uint32_t)(i & 7) * 8;
+        return sh ? (a >> sh) | (b << (64 - sh)) : a;
+    }
+    __device__ __forceinline__ uint64_t word(uint64_t i) const {   // bytes i..i+7, all < len
+        if (i >= plen1) return key_word(i - plen1);
+        uint64_t w = pre_word(i);
+        const uint32_t kb = plen1 - (uint32_t)i;        // prefix bytes in this word
+        if (kb < 8) {                                   // key bytes 0 .. 7-kb (< len)
+            uint64_t k;
+            if constexpr (kLds) {
+                k = key_word(0);                        // LDS bytes past them shift out
+            } else {
+                k = 0;
+                for (uint32_t j = 0; j < 8 - kb; ++j) k |= (uint64_t)g[j] << (8 * j);
+            }
+            w |= k << (8 * kb);
+        }
+        return w;
+    }
+    __device__ __forceinline__ uint32_t word32(uint64_t i) const {  // bytes i..i+3, all < len
+        if (i >= plen1) {
+            if constexpr (kLds) return (uint32_t)key_word(i - plen1);  // LDS reads past the key stay in the pad
+        } else if (plen1 - i >= 4) {
+            return (uint32_t)pre_word(i);
+        }
+        uint32_t w = 0;
+        for (int k = 0; k < 4; ++k) w |= (uint32_t)byte(i + k) << (8 * k);
+        return w;
+    }
+};
+
+template <bool kLds>
+__device__ uint64_t xxh64(const Formatted<kLds>& f, uint64_t len, uint64_t seed) {
+    uint64_t h, p = 0;
+    if (len >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        for (; p + 32 <= len; p += 32) {
+            v1 = xround(v1, f.word(p));
+            v2 = xround(v2, f.word(p + 8));
+            v3 = xround(v3, f.word(p + 16));
+            v4 = xround(v4, f.word(p + 24));
+        }
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        h = xmerge(h, v1);
+        h = xmerge(h, v2);
+        h = xmerge(h, v3);
+        h = xmerge(h, v4);
+    } else {
+        h = seed + P5;
+    }
+    h += len;
+    for (; p + 8 <= len; p += 8) h = rotl(h ^ xround(0, f.word(p)), 27) * P1 + P4;
+    if (p + 4 <= len) {
+        h = rotl(h ^ ((uint64_t)f.word32(p) * P1), 23) * P2 + P3;
+        p += 4;
+    }
+    for (; p < len; ++p) h = rotl(h ^ ((uint64_t)f.byte(p) * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
+__device__ __forceinline__ uint64_t finish_id(uint64_t h) { return h == RL_KEY_RESERVED ? RL_KEY_RESERVED - 1 : h; }
+
+__global__ __launch_bounds__(KH_BLOCK) void k_key_hash(const uint8_t* __restrict__ bytes, uint64_t nbytes,
+                                                        const uint64_t* __restrict__ offsets, uint64_t m,
+                                                        uint64_t seed, Prefix pre, uint64_t* __restrict__ key_id) {
+    __shared__ uint64_t s_raw[KH_RAW_WORDS + 2];
+    __shared__ uint64_t s_pre64[KH_PRE_BYTES / 8 + 1];
+    __shared__ uint64_t s_off[KH_BLOCK + 1];
+
+    const uint64_t b0 = (uint64_t)blockIdx.x * KH_BLOCK;
+    const uint32_t nk = (uint32_t)min<uint64_t>(KH_BLOCK, m - b0);
+    const uint32_t t = threadIdx.x;
+    uint8_t* s_pre = reinterpret_cast<uint8_t*>(s_pre64);
+
+    for (uint32_t i = t; i <= nk; i += KH_BLOCK) s_off[i] = offsets[b0 + i];
+    for (uint32_t i = t; i < KH_PRE_BYTES; i += KH_BLOCK) s_pre[i] = pre.b[i];
+    __syncthreads();
+
+    // the group's byte range, from an aligned base; offsets out of order or past
+    // nbytes make the range unusable (those keys get RL_KEY_RESERVED below)
+    uint64_t lo = s_off[0], hi = s_off[nk];
+    const bool range_ok = lo <= hi && hi <= nbytes;
+    const uint64_t base = lo & ~(uint64_t)15;
+    const uint64_t span = range_ok ? hi - base : 0;
+    const bool fits = range_ok && span <= KH_RAW_BYTES;
+    const bool aligned = ((uintptr_t)bytes & 15) == 0;
+    if (fits) {
+        const uint64_t nchunk = (span + 15) / 16;
+        for (uint64_t c = t; c < nchunk; c += KH_BLOCK) {
+            uint64_t g = base + c * 16;
+            uint64_t w0, w1;
+            if (aligned && g + 16 <= nbytes) {
+                ulonglong2 v = *reinterpret_cast<const ulonglong2*>(bytes + g);   // bytes, base, g 16-aligned
+                w0 = v.x;
+                w1 = v.y;
+            } else {                                        // the buffer's ragged tail, or an unaligned buffer
+                w0 = w1 = 0;
+                for (int k = 0; k < 16 && g + k < nbytes; ++k)
+                    (k < 8 ? w0 : w1) |= (uint64_t)bytes[g + k] << (8 * (k & 7));
+            }
+            s_raw[2 * c] = w0;
+            s_raw[2 * c + 1] = w1;
+        }
+        if (t == 0) s_raw[2 * nchunk] = s_raw[2 * nchunk + 1] = 0;   // funnel pad (never used as key bytes)
+    }
+    __syncthreads();
+    if (t >= nk) return;
+
+    const uint64_t a = s_off[t], z = s_off[t + 1];
+    uint64_t id;
+    if (!(a <= z && z <= nbytes)) {
+        id = RL_KEY_RESERVED;
+    } else {
+        const uint64_t len = pre.len1 + (z - a);
+        if (fits && a >= lo && z <= hi) {   // inside the staged range
+            Formatted<true> f{s_pre, pre.len1, s_raw, (uint32_t)(a - base), nullptr};
+            id = finish_id(xxh64(f, len, seed));
+        } else {
+            Formatted<false> f{s_pre, pre.len1, nullptr, 0, bytes + a};
+            id = finish_id(xxh64(f, len, seed));
+        }
+    }
+    key_id[b0 + t] = id;
+}
+
+int make_prefix(const char* prefix, size_t prefix_len, Prefix* out) {
+    if (prefix_len > RL_KEYHASH_MAX_PREFIX || (prefix_len && !prefix)) return RL_EINVAL;
+    std::memset(out, 0, sizeof *out);
+    if (prefix_len) {
+        std::memcpy(out->b, prefix, prefix_len);
+        out->b[prefix_len] = ':';
+        out->len1 = (uint32_t)prefix_len + 1;
+    }
+    return RL_OK;
+}
+
+}  // namespace
+
+extern "C" int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
+                                   uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id,
+                                   void* stream) {
+    Prefix pre;
+    if (make_prefix(prefix, prefix_len, &pre) != RL_OK) return RL_EINVAL;
+    if (m == 0) return RL_OK;
+    if (!offsets || !key_id || (nbytes && !bytes)) return RL_EINVAL;
+    if (m > ((uint64_t)1 << 40)) return RL_EINVAL;
+    const uint64_t blocks = (m + KH_BLOCK - 1) / KH_BLOCK;
+    hipLaunchKernelGGL(k_key_hash, dim3((uint32_t)blocks), dim3(KH_BLOCK), 0, (hipStream_t)stream, bytes, nbytes,
+                       offsets, (uint64_t)m, seed, pre, key_id);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+extern "C" int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
+                            uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id) {
+    Prefix pre;
+    if (make_prefix(prefix, prefix_len, &pre) != RL_OK) return RL_EINVAL;
+    if (m == 0) return RL_OK;
+    if (!offsets || !key_id || (nbytes && !bytes)) return RL_EINVAL;
+    for (size_t i = 0; i < m; ++i)
+        if (offsets[i] > offsets[i + 1]) return RL_EINVAL;
+    if (offsets[m] > nbytes) return RL_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return RL_EDEVICE;
+    uint8_t* d_bytes = nullptr;
+    uint64_t *d_off = nullptr, *d_id = nullptr;
+    int rc = RL_OK;
+    const uint64_t nb = nbytes ? nbytes : 1;
+    if (hipMalloc(&d_bytes, nb) != hipSuccess || hipMalloc(&d_off, (m + 1) * 8) != hipSuccess ||
+        hipMalloc(&d_id, m * 8) != hipSuccess) {
+        rc = RL_ENOMEM;
+    } else if ((nbytes && hipMemcpy(d_bytes, bytes, nbytes, hipMemcpyHostToDevice) != hipSuccess) ||
+               hipMemcpy(d_off, offsets, (m + 1) * 8, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = RL_EDEVICE;
+    } else if ((rc = rl_hash_keys_device(m, d_bytes, nbytes, d_off, seed, prefix, prefix_len, d_id, nullptr)) ==
+               RL_OK) {
+        if (hipMemcpy(key_id, d_id, m * 8, hipMemcpyDeviceToHost) != hipSuccess) rc = RL_EDEVICE;
+    }
+    (void)hipFree(d_bytes);
+    (void)hipFree(d_off);
+    (void)hipFree(d_id);
+    return rc;
+}

@@ -141,6 +141,8 @@ _sig = {
     "rl_coalescer_wait": (C.c_int, [vp, C.c_uint64, C.c_int64, vp, vp, vp, vp]),
     "rl_coalescer_decide": (C.c_int, [vp, C.c_uint64, C.c_int64, C.c_int64, C.c_uint32, vp, vp, vp, vp]),
     "rl_coalescer_get_stats": (C.c_int, [vp, C.POINTER(rl_coalescer_stats)]),
+    "rl_hash_keys_device": (C.c_int, [C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_size_t, vp, vp]),
+    "rl_hash_keys": (C.c_int, [C.c_int32, C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_size_t, vp]),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -289,6 +291,29 @@ class Engine:
 
 
 # --- host mirror of the Go API (include/rl_limiter.h) ------------------------
+
+def pack_keys(keys) -> tuple[np.ndarray, np.ndarray]:
+    """Concatenate raw keys (bytes / str) into (bytes u8, offsets u64[m+1])."""
+    bs = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    if bs:
+        off[1:] = np.cumsum([len(b) for b in bs], dtype=np.uint64)
+    return np.frombuffer(b"".join(bs), dtype=np.uint8).copy(), off
+
+
+def hash_keys(keys_or_packed, seed: int, prefix: bytes | str = b"", device=0, check=True) -> np.ndarray:
+    """On-GPU FormatKey + XXH64 (include/rl_keyhash.h): key ids for rl_decide_batch."""
+    data, off = keys_or_packed if isinstance(keys_or_packed, tuple) else pack_keys(keys_or_packed)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    pre = prefix.encode() if isinstance(prefix, str) else bytes(prefix)
+    m = len(off) - 1
+    out = np.zeros(max(m, 0), dtype=np.uint64)
+    rc = lib.rl_hash_keys(device, m, _ptr(data), data.size, _ptr(off), seed, pre, len(pre), _ptr(out))
+    if check and rc != RL_OK:
+        raise EngineError(rc, "rl_hash_keys failed")
+    return out if check else (rc, out)
+
 
 def config_validate(algorithm, limit, window_ns):
     """Config.Validate(); algorithm None == nil *Config.  Returns '' or the message."""

@@ -1,0 +1,57 @@
+/*
+ * rl_keyhash.h -- on-GPU key formatting + hashing.
+ *
+ * The reference names every Redis key with string building on the host:
+ *   Config.FormatKey            config.go:81-87     prefix + ":" + key ("" -> key)
+ *   tokenBucketLimiter.AllowN   tokenbucket.go:95   redisKey := t.config.FormatKey(key)
+ *   fixedWindowLimiter.formatKey fixedwindow.go:139-141  Sprintf("%s:%d", FormatKey(key), ws)
+ *   slidingWindowLimiter.formatKey slidingwindow.go:150-152
+ * Redis then looks the string up in its keyspace.  Here the window suffix is
+ * already handled by the engine (state entries keyed by the base key carry
+ * their window ids), so the only string work left is FormatKey plus the
+ * keyspace lookup.  These entry points take a batch of raw user keys (one
+ * concatenated byte buffer + offsets), form `prefix ":" key` on the device and
+ * hash it with XXH64 (seed = the limiter's namespace), producing the key_id
+ * array rl_decide_batch[_device] consumes (include/rl_engine.h).
+ *
+ *   key_id[i] = XXH64(FormatKey(prefix, bytes[offsets[i] .. offsets[i+1])), seed)
+ *               (RL_KEY_RESERVED is mapped to RL_KEY_RESERVED - 1)
+ *
+ * Identity: distinct formatted keys share state only on a 64-bit hash
+ * collision (probability ~ k^2 / 2^65 over k live keys: 3e-8 at 1M keys,
+ * 2.7e-2 at 1e9).  Callers that need exact identity at 1e9 keys keep the
+ * host interner of include/rl_limiter.h.
+ *
+ * Errors: RL_EINVAL for a prefix longer than RL_KEYHASH_MAX_PREFIX bytes, a
+ * NULL array with m > 0, or (host entry point) offsets that decrease or run
+ * past nbytes.  The device entry point cannot check offsets without a sync:
+ * a request whose offsets are out of order or past nbytes gets
+ * RL_KEY_RESERVED, which rl_decide_batch reports as RL_INVALID.
+ */
+#ifndef RL_KEYHASH_H
+#define RL_KEYHASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RL_KEYHASH_MAX_PREFIX 240
+
+/* Device arrays, enqueued on `stream` (a hipStream_t; NULL = the null stream).
+ * bytes: nbytes readable bytes; offsets: m + 1 entries. */
+int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
+                        uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id,
+                        void* stream);
+
+/* Host arrays on device `device`: copies in, hashes, copies out.  Synchronous. */
+int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
+                 uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RL_KEYHASH_H */

@@ -23,7 +23,7 @@ os.makedirs(dst, exist_ok=True)
 
 
 def short(name):
-    name = name.split("(")[0]
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
     return name.replace("void ", "").replace("rl::", "")
 
 
@@ -38,7 +38,7 @@ for kind in ("fetch", "write"):
         pmc[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
 
 lines = [f"# rocprofv3 summary: {tag}", "",
-         "Command: `scripts/profile.sh` (bench.py, " + os.environ.get("BARGS", "--steps 10 --warmup 2") + ")", "",
+         os.environ.get("PROF_CMD") or ("Command: `scripts/profile.sh` (bench.py, " + os.environ.get("BARGS", "--steps 10 --warmup 2") + ")"), "",
          "| kernel | calls | avg us | % | FETCH_SIZE KiB/launch | 2xFETCH MB | WRITE_SIZE MB |",
          "|---|---|---|---|---|---|---|"]
 for r in stats:
@@ -65,4 +65,6 @@ for r in stats:
                       "fetch_x2_bytes": 2 * sum(f) / len(f) * 1024, "write_bytes": sum(w) / len(w) * 1024,
                       "avg_ns": float(r["AverageNs"])}
 if traffic:   # a trace-only run (NO_PMC) keeps the last PMC passes' numbers
-    json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+    # profiles/traffic.json feeds bench.py's roofline: only bench.py profiles write it
+    name = "traffic.json" if not os.environ.get("PROF_CMD") else tag + "_traffic.json"
+    json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, name), "w"), indent=1)

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("rl_engine.h", "rl_limiter.h", "rl_coalescer.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("rl_engine.h", "rl_limiter.h", "rl_coalescer.h", "rl_keyhash.h")]
 
 
 def declared_functions():
