@@ -120,6 +120,9 @@ def main():
     ap.add_argument("--route", action="store_true",
                     help="routed ingress: every rank draws keys from the whole key space and an RCCL "
                          "all-to-all moves each request to its owner GPU and the result back")
+    ap.add_argument("--string-keys", action="store_true",
+                    help="requests carry raw string keys ('user:<rank>:<12 hex>'): every step runs the on-GPU "
+                         "FormatKey + XXH64 (rl_hash_keys_device, prefix 'ratelimit') before the decisions")
     ap.add_argument("--e2e", action="store_true",
                     help="configs[4]: open-loop Zipf 1.5 traffic through the request coalescer at fixed QPS "
                          "levels (lib/rl_bench_e2e); reports per-request latency percentiles")
@@ -163,6 +166,18 @@ def main():
             torch.from_numpy(n).to(dev),
             torch.from_numpy(cfg.view(np.int32)).to(dev),
         ))
+    key_strings = []
+    if args.string_keys:
+        # fixed-width raw keys 'user:RR:xxxxxxxxxxxx' (20 B), built vectorized
+        hexd = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+        head = np.frombuffer(f"user:{rank % 100:02d}:".encode(), dtype=np.uint8)
+        for key, _, _, _ in host:
+            sh = np.arange(44, -4, -4, dtype=np.uint64)
+            digits = hexd[((key[:, None] >> sh[None, :]) & np.uint64(15)).astype(np.int64)]
+            raw = np.concatenate([np.broadcast_to(head, (key.size, head.size)), digits], axis=1)
+            off = np.arange(key.size + 1, dtype=np.int64) * raw.shape[1]
+            key_strings.append((torch.from_numpy(np.ascontiguousarray(raw).reshape(-1)).to(dev),
+                                torch.from_numpy(off).to(dev), None))
     del host
 
     algs = {a for a, _, _ in gen.configs}
@@ -195,6 +210,16 @@ def main():
         if args.route:
             import shard
             shard.route_and_decide_torch(k, t, n, c, decide_owned)
+            return
+        if args.string_keys:
+            # raw keys: hashed on the engine's grouping stream ahead of the probe
+            raw, off, _ = key_strings[b]
+            rc = rl_amd.lib.rl_decide_batch_keys_device(
+                eng.h, m, raw.data_ptr(), raw.numel(), off.data_ptr(), 1, b"ratelimit", 9, t.data_ptr(),
+                n.data_ptr(), c.data_ptr(), None, out_dec.data_ptr(), out_rem.data_ptr(), out_retry.data_ptr(),
+                out_reset.data_ptr(), out_tok.data_ptr(), stream)
+            if rc != 0:
+                raise SystemExit(f"rl_decide_batch_keys_device: {rc}")
             return
         eng.decide_device(m, k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
                           out_dec.data_ptr(), out_rem.data_ptr(), out_retry.data_ptr(), out_reset.data_ptr(),
@@ -311,7 +336,9 @@ def main():
         "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
         "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
                    "profile": "redis7 (Lua %.14g state round trip)", "parallelism": (f"routed all-to-all x{world}" if args.route else f"key-shard x{world}"),
-                   "batches_in_flight": 1 if args.no_pipeline or args.route else 3},
+                   "batches_in_flight": 1 if args.no_pipeline or args.route else 3,
+                   "keys": ("raw strings, on-GPU FormatKey + XXH64 in every step" if args.string_keys
+                            else "integer key ids")},
         "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": bytes_per_dec * m,

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/rl_engine.h"
+#include "../../include/rl_keyhash.h"
 #include "rl_replay.h"
 #include "rl_semantics.h"
 #include "rl_sort.h"
@@ -342,6 +343,7 @@ struct BatchSet {
     uint32_t* status = nullptr;
     uint32_t* claim = nullptr;
     hipEvent_t front_done = nullptr, chain_done = nullptr, back_done = nullptr;
+    uint64_t* kid = nullptr;      // key ids hashed from raw keys (rl_decide_batch_keys_device; lazy)
     bool used = false;
 };
 
@@ -439,6 +441,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.q_add); (void)hipFree(B.q_th); (void)hipFree(B.q_lq); (void)hipFree(B.q_when);
     (void)hipFree(B.runs.len); (void)hipFree(B.runs.E); (void)hipFree(B.runs.D0); (void)hipFree(B.runs.D1);
     (void)hipFree(B.zero);
+    (void)hipFree(B.kid);
     if (B.front_done) (void)hipEventDestroy(B.front_done);
     if (B.back_done) (void)hipEventDestroy(B.back_done);
     if (B.chain_done) (void)hipEventDestroy(B.chain_done);
@@ -677,14 +680,31 @@ static hipEvent_t take_event(rl_engine* e) {
     return ev;
 }
 
+// raw keys of one chunk (rl_decide_batch_keys_device): hashed into key ids on
+// the stream that runs the chunk's grouping, ahead of k_probe / k_small
+struct KeyBytes {
+    const uint8_t* bytes;
+    uint64_t nbytes;
+    const uint64_t* offsets;      // this chunk's m + 1 offsets (absolute into bytes)
+    uint64_t seed;
+    const char* prefix;
+    size_t prefix_len;
+};
+
 // enqueue one batch of m <= max_batch requests (see BatchSet); s waits for
 // its finish.  inputs_ready: the caller guarantees the input arrays are
 // complete now (RL_OPT_PIPELINE); otherwise the grouping waits for s.
-static int run_small(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, bool inputs_ready) {
+static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool inputs_ready, const KeyBytes* kb) {
     hipStream_t c = e->chain;   // after every earlier replay (table state)
     if (!inputs_ready) {
         HIPCHK(e, hipEventRecord(e->ev_in, s));
         HIPCHK(e, hipStreamWaitEvent(c, e->ev_in, 0));
+    }
+    if (kb) {   // d_key: the host API's staging, free while the device API runs (not re-entrant)
+        int r = rl_hash_keys_device(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, kb->prefix, kb->prefix_len,
+                                    e->d_key, c);
+        if (r != RL_OK) return r;
+        a.key = e->d_key;
     }
     ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, e->s_sms, e->s_dec, e->s_rem, e->s_retry, e->s_reset, e->s_tok};
     TbPre pre{e->s_add, e->s_th, e->s_reset, e->s_lq, e->s_when};
@@ -699,9 +719,10 @@ static int run_small(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
     return RL_OK;
 }
 
-static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, bool inputs_ready) {
+static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool inputs_ready,
+                     const KeyBytes* kb = nullptr) {
     if (m == 0) return RL_OK;
-    if (m <= e->small_max && !e->timing) return run_small(e, m, a, s, inputs_ready);
+    if (m <= e->small_max && !e->timing) return run_small(e, m, a, s, inputs_ready, kb);
     BatchSet& B = e->set[e->next_set];
     e->last_set = e->next_set;
     e->next_set = (e->next_set + 1) % NSETS;
@@ -711,6 +732,13 @@ static int run_batch(rl_engine* e, uint32_t m, const ReqArgs& a, hipStream_t s, 
         HIPCHK(e, hipStreamWaitEvent(f, e->ev_in, 0));
     }
     if (B.used) HIPCHK(e, hipStreamWaitEvent(f, B.back_done, 0));   // set reuse
+    if (kb) {
+        if (!B.kid && hipMalloc(&B.kid, 8 * (size_t)e->max_batch) != hipSuccess) return RL_ENOMEM;
+        int r = rl_hash_keys_device(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, kb->prefix, kb->prefix_len,
+                                    B.kid, f);
+        if (r != RL_OK) return r;
+        a.key = B.kid;
+    }
     std::array<hipEvent_t, 8> ev{};
     if (e->timing) {
         for (auto& x : ev) x = take_event(e);
@@ -852,6 +880,30 @@ extern "C" int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* ke
                   decision + off, remaining + off, retry_after_ns + off, reset_at_ns + off,
                   tokens ? tokens + off : nullptr};
         int r = run_batch(e, c, a, s, (e->flags & RL_OPT_PIPELINE) != 0);
+        if (r != RL_OK) return r;
+    }
+    return RL_OK;
+}
+
+extern "C" int rl_decide_batch_keys_device(rl_engine* e, size_t m, const uint8_t* key_bytes, uint64_t nbytes,
+                                           const uint64_t* key_offsets, uint64_t seed, const char* prefix,
+                                           size_t prefix_len, const int64_t* ts_ns, const int64_t* n,
+                                           const uint32_t* cfg_id, const int64_t* server_ms, uint8_t* decision,
+                                           int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns,
+                                           double* tokens, void* stream) {
+    if (!e || prefix_len > RL_KEYHASH_MAX_PREFIX || (prefix_len && !prefix) ||
+        (m && (!key_offsets || (nbytes && !key_bytes) || !ts_ns || !n || !cfg_id || !decision || !remaining ||
+               !retry_after_ns || !reset_at_ns)))
+        return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    for (size_t off = 0; off < m; off += e->max_batch) {
+        uint32_t c = (uint32_t)std::min<size_t>(e->max_batch, m - off);
+        ReqArgs a{nullptr, ts_ns + off, n + off, cfg_id + off, server_ms ? server_ms + off : nullptr,
+                  decision + off, remaining + off, retry_after_ns + off, reset_at_ns + off,
+                  tokens ? tokens + off : nullptr};
+        KeyBytes kb{key_bytes, nbytes, key_offsets + off, seed, prefix, prefix_len};
+        int r = run_batch(e, c, a, s, (e->flags & RL_OPT_PIPELINE) != 0, &kb);
         if (r != RL_OK) return r;
     }
     return RL_OK;

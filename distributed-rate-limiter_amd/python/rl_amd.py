@@ -142,6 +142,8 @@ _sig = {
     "rl_coalescer_decide": (C.c_int, [vp, C.c_uint64, C.c_int64, C.c_int64, C.c_uint32, vp, vp, vp, vp]),
     "rl_coalescer_get_stats": (C.c_int, [vp, C.POINTER(rl_coalescer_stats)]),
     "rl_hash_keys_device": (C.c_int, [C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_size_t, vp, vp]),
+    "rl_decide_batch_keys_device": (C.c_int, [vp, C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p,
+                                              C.c_size_t] + [vp] * 10),
     "rl_hash_keys": (C.c_int, [C.c_int32, C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_size_t, vp]),
 }
 for _name, (_res, _args) in _sig.items():

@@ -34,6 +34,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "rl_engine.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -49,6 +51,17 @@ int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbytes, const u
 /* Host arrays on device `device`: copies in, hashes, copies out.  Synchronous. */
 int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
                  uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id);
+
+/* rl_decide_batch_device (include/rl_engine.h) with raw keys instead of key
+ * ids: the hashing above runs on the engine's grouping stream ahead of the
+ * table probe, so batches stay pipelined (RL_OPT_PIPELINE).  key_bytes /
+ * key_offsets are device arrays under the same completeness rule as the other
+ * inputs; offsets are absolute into key_bytes (m + 1 entries). */
+int rl_decide_batch_keys_device(rl_engine* e, size_t m, const uint8_t* key_bytes, uint64_t nbytes,
+                                const uint64_t* key_offsets, uint64_t seed, const char* prefix, size_t prefix_len,
+                                const int64_t* ts_ns, const int64_t* n, const uint32_t* cfg_id,
+                                const int64_t* server_ms, uint8_t* decision, int64_t* remaining,
+                                int64_t* retry_after_ns, int64_t* reset_at_ns, double* tokens, void* stream);
 
 #ifdef __cplusplus
 }

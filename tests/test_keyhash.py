@@ -181,3 +181,52 @@ def test_gpu_decisions_through_hashed_ids(rl, alg):
     assert np.array_equal(got.remaining, rem)
     assert np.array_equal(got.retry_after_ns, retry)
     assert np.array_equal(got.reset_at_ns, reset)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_gpu_decide_batch_keys_device(rl, pipeline):
+    """rl_decide_batch_keys_device (hash on the grouping stream) == oracle with
+    string identity, over big and small batches, batches in flight, chunking."""
+    import torch
+
+    import oracle
+    from tracegen import NS, T0
+    rng = np.random.default_rng(21 + pipeline)
+    names = [f"tenant:{i}:{'x' * (i % 37)}".encode() for i in range(30_000)]
+    sizes = [50_000, 3000, 70_000, 17, 40_000]
+    eng = rl.Engine(profile=rl.PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16, max_batch=1 << 15,
+                    flags=rl.OPT_PIPELINE if pipeline else 0)
+    sim = oracle.OracleSim(oracle.REDIS7)
+    cfgs = [(1, 20, 12 * NS), (2, 30, 3 * NS), (3, 40, 2 * NS)]
+    for a, L, W in cfgs:
+        assert eng.register(a, L, W) == sim.add_config(a, L, W)
+    dev = torch.device("cuda", 0)
+    t_last = T0
+    pending = []
+    for m in sizes:
+        pick = np.minimum(rng.zipf(1.2, m) - 1, len(names) - 1)
+        data, off = rl.pack_keys([names[i] for i in pick])
+        ts = t_last + np.cumsum(rng.integers(0, 200_000, m)).astype(np.int64)
+        t_last = int(ts[-1])
+        n = rng.choice([1, 1, 1, 3], m).astype(np.int64)
+        cfg = (pick % 3).astype(np.uint32)
+        d = [torch.from_numpy(x).to(dev) for x in (data, off.view(np.int64), ts, n, cfg.view(np.int32))]
+        o = [torch.empty(m, dtype=torch.uint8, device=dev)] + \
+            [torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)] + \
+            [torch.empty(m, dtype=torch.float64, device=dev)]
+        torch.cuda.synchronize()   # inputs complete before the call (RL_OPT_PIPELINE contract)
+        rc = rl.lib.rl_decide_batch_keys_device(eng.h, m, d[0].data_ptr(), data.size, d[1].data_ptr(), 4,
+                                                b"ratelimit", 9, d[2].data_ptr(), d[3].data_ptr(),
+                                                d[4].data_ptr(), None, *[x.data_ptr() for x in o], None)
+        assert rc == rl.RL_OK
+        # string identity for the oracle: the name index, one namespace per config
+        pending.append((d, o, sim.decide(pick.astype(np.uint64) * 4 + cfg, ts, n, cfg)))
+    assert eng.sync() == rl.RL_OK
+    torch.cuda.synchronize()
+    for d, o, (dec, rem, retry, reset, tok) in pending:
+        assert np.array_equal(o[0].cpu().numpy(), dec)
+        assert np.array_equal(o[1].cpu().numpy(), rem)
+        assert np.array_equal(o[2].cpu().numpy(), retry)
+        assert np.array_equal(o[3].cpu().numpy(), reset)
+    eng.close()
