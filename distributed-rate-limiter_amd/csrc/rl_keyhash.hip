@@ -22,7 +22,10 @@
 namespace {
 
 constexpr int KH_BLOCK = 256;                 // keys per workgroup (4 waves)
-constexpr int KH_RAW_BYTES = 24576;           // staged key bytes per workgroup
+#ifndef RL_KH_RAW_BYTES
+#define RL_KH_RAW_BYTES 24576
+#endif
+constexpr int KH_RAW_BYTES = RL_KH_RAW_BYTES;  // staged key bytes per workgroup
 constexpr int KH_RAW_WORDS = KH_RAW_BYTES / 8;
 constexpr int KH_PRE_BYTES = 256;             // prefix + ':' (<= 241 bytes used)
 
