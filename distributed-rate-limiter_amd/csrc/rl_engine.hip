@@ -401,6 +401,7 @@ struct rl_engine {
 
     // host-API staging (device side)
     uint64_t* d_key = nullptr;
+    uint64_t* small_kid = nullptr;   // key ids hashed for k_small (rl_decide_batch_keys_device; lazy)
     int64_t *d_ts = nullptr, *d_n = nullptr, *d_sms = nullptr;
     uint32_t* d_cfgid = nullptr;
     uint8_t* d_dec = nullptr;
@@ -495,6 +496,7 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_win);
     for (auto& B : e->set) free_set(B);
     (void)hipFree(e->d_eflags);
+    (void)hipFree(e->small_kid);
     (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
     (void)hipFree(e->d_dec); (void)hipFree(e->d_rem); (void)hipFree(e->d_retry); (void)hipFree(e->d_reset); (void)hipFree(e->d_tok);
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -700,11 +702,12 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         HIPCHK(e, hipEventRecord(e->ev_in, s));
         HIPCHK(e, hipStreamWaitEvent(c, e->ev_in, 0));
     }
-    if (kb) {   // d_key: the host API's staging, free while the device API runs (not re-entrant)
+    if (kb) {   // own buffer, ordered on c: written by the hash, read by k_small
+        if (!e->small_kid && hipMalloc(&e->small_kid, 8 * (size_t)e->small_max) != hipSuccess) return RL_ENOMEM;
         int r = rl_hash_keys_device(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, kb->prefix, kb->prefix_len,
-                                    e->d_key, c);
+                                    e->small_kid, c);
         if (r != RL_OK) return r;
-        a.key = e->d_key;
+        a.key = e->small_kid;
     }
     ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, e->s_sms, e->s_dec, e->s_rem, e->s_retry, e->s_reset, e->s_tok};
     TbPre pre{e->s_add, e->s_th, e->s_reset, e->s_lq, e->s_when};
