@@ -233,7 +233,7 @@ extern "C" int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbyt
     if (make_prefix(prefix, prefix_len, &pre) != RL_OK) return RL_EINVAL;
     if (m == 0) return RL_OK;
     if (!offsets || !key_id || (nbytes && !bytes)) return RL_EINVAL;
-    if (m > ((uint64_t)1 << 40)) return RL_EINVAL;
+    if (m > ((uint64_t)1 << 37)) return RL_EINVAL;   // grid of <= 2^31 one-wave groups
     // group size from the mean key length (10 % headroom: a 256-key group's
     // byte count varies little around 256 x the mean)
     const bool wide = (double)nbytes / (double)m * 1.1 > (double)KH_RAW_BYTES / 256.0 - 1.0;

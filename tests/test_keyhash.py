@@ -230,3 +230,12 @@ def test_gpu_decide_batch_keys_device(rl, pipeline):
         assert np.array_equal(o[2].cpu().numpy(), retry)
         assert np.array_equal(o[3].cpu().numpy(), reset)
     eng.close()
+
+
+def test_decide_batch_keys_device_argument_errors(rl):
+    # rejected before any device call (no GPU needed)
+    vp = None
+    assert rl.lib.rl_decide_batch_keys_device(None, 0, vp, 0, vp, 0, None, 0, *([vp] * 10)) == rl.RL_EINVAL
+    assert rl.lib.rl_hash_keys_device(1, vp, 0, vp, 0, None, 0, vp, vp) == rl.RL_EINVAL        # NULL offsets
+    assert rl.lib.rl_hash_keys_device(0, vp, 0, vp, 0, b"p" * 241, 241, vp, vp) == rl.RL_EINVAL  # prefix too long
+    assert rl.lib.rl_hash_keys_device(0, vp, 0, vp, 0, None, 0, vp, vp) == rl.RL_OK             # empty batch
