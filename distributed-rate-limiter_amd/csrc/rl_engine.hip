@@ -691,7 +691,13 @@ struct KeyBytes {
     uint64_t seed;
     const char* prefix;
     size_t prefix_len;
+    double mean_len;              // the whole batch's mean key length (group size choice)
 };
+
+// rl_keyhash.hip
+int rl_hash_keys_launch(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets, uint64_t seed,
+                        const uint32_t* cfg, const char* prefix, size_t prefix_len, double mean_len,
+                        uint64_t* key_id, void* stream);
 
 // enqueue one batch of m <= max_batch requests (see BatchSet); s waits for
 // its finish.  inputs_ready: the caller guarantees the input arrays are
@@ -704,8 +710,8 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     }
     if (kb) {   // own buffer, ordered on c: written by the hash, read by k_small
         if (!e->small_kid && hipMalloc(&e->small_kid, 8 * (size_t)e->small_max) != hipSuccess) return RL_ENOMEM;
-        int r = rl_hash_keys_device(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, kb->prefix, kb->prefix_len,
-                                    e->small_kid, c);
+        int r = rl_hash_keys_launch(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, a.cfg, kb->prefix,
+                                    kb->prefix_len, kb->mean_len, e->small_kid, c);
         if (r != RL_OK) return r;
         a.key = e->small_kid;
     }
@@ -737,8 +743,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (B.used) HIPCHK(e, hipStreamWaitEvent(f, B.back_done, 0));   // set reuse
     if (kb) {
         if (!B.kid && hipMalloc(&B.kid, 8 * (size_t)e->max_batch) != hipSuccess) return RL_ENOMEM;
-        int r = rl_hash_keys_device(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, kb->prefix, kb->prefix_len,
-                                    B.kid, f);
+        int r = rl_hash_keys_launch(m, kb->bytes, kb->nbytes, kb->offsets, kb->seed, a.cfg, kb->prefix,
+                                    kb->prefix_len, kb->mean_len, B.kid, f);
         if (r != RL_OK) return r;
         a.key = B.kid;
     }
@@ -905,7 +911,7 @@ extern "C" int rl_decide_batch_keys_device(rl_engine* e, size_t m, const uint8_t
         ReqArgs a{nullptr, ts_ns + off, n + off, cfg_id + off, server_ms ? server_ms + off : nullptr,
                   decision + off, remaining + off, retry_after_ns + off, reset_at_ns + off,
                   tokens ? tokens + off : nullptr};
-        KeyBytes kb{key_bytes, nbytes, key_offsets + off, seed, prefix, prefix_len};
+        KeyBytes kb{key_bytes, nbytes, key_offsets + off, seed, prefix, prefix_len, (double)nbytes / (double)m};
         int r = run_batch(e, c, a, s, (e->flags & RL_OPT_PIPELINE) != 0, &kb);
         if (r != RL_OK) return r;
     }

@@ -152,7 +152,8 @@ __device__ __forceinline__ uint64_t finish_id(uint64_t h) { return h == RL_KEY_R
 template <int KH_BLOCK>   // keys per workgroup = threads (256: 4 waves, 64: one wave)
 __global__ __launch_bounds__(KH_BLOCK) void k_key_hash(const uint8_t* __restrict__ bytes, uint64_t nbytes,
                                                         const uint64_t* __restrict__ offsets, uint64_t m,
-                                                        uint64_t seed, Prefix pre, uint64_t* __restrict__ key_id) {
+                                                        uint64_t seed, const uint32_t* __restrict__ cfg, Prefix pre,
+                                                        uint64_t* __restrict__ key_id) {
     __shared__ uint64_t s_raw[KH_RAW_WORDS + 2];
     __shared__ uint64_t s_pre64[KH_PRE_BYTES / 8 + 1];
     __shared__ uint64_t s_off[KH_BLOCK + 1];
@@ -197,6 +198,7 @@ __global__ __launch_bounds__(KH_BLOCK) void k_key_hash(const uint8_t* __restrict
     if (t >= nk) return;
 
     const uint64_t a = s_off[t], z = s_off[t + 1];
+    if (cfg) seed = RL_CFG_SEED(seed, cfg[b0 + t]);   // one namespace per config
     uint64_t id;
     if (!(a <= z && z <= nbytes)) {
         id = RL_KEY_RESERVED;
@@ -226,27 +228,40 @@ int make_prefix(const char* prefix, size_t prefix_len, Prefix* out) {
 
 }  // namespace
 
-extern "C" int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
-                                   uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id,
-                                   void* stream) {
+// The launch behind rl_hash_keys_device and the engine's raw-key path.
+// mean_len: mean key length (bytes) that picks the group size -- the engine
+// passes the whole batch's mean, so the chunks of a batch larger than
+// max_batch choose as the batch does.  cfg (nullable): per-request config ids
+// mixed into the seed (rl_cfg_seed).  The HSA grid is a 32-bit work-item count,
+// so m is capped below 2^32 work-items.
+int rl_hash_keys_launch(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets, uint64_t seed,
+                        const uint32_t* cfg, const char* prefix, size_t prefix_len, double mean_len,
+                        uint64_t* key_id, void* stream) {
     Prefix pre;
     if (make_prefix(prefix, prefix_len, &pre) != RL_OK) return RL_EINVAL;
     if (m == 0) return RL_OK;
     if (!offsets || !key_id || (nbytes && !bytes)) return RL_EINVAL;
-    if (m > ((uint64_t)1 << 37)) return RL_EINVAL;   // grid of <= 2^31 one-wave groups
+    if (m > RL_KEYHASH_MAX_KEYS) return RL_EINVAL;
     // group size from the mean key length (10 % headroom: a 256-key group's
     // byte count varies little around 256 x the mean)
-    const bool wide = (double)nbytes / (double)m * 1.1 > (double)KH_RAW_BYTES / 256.0 - 1.0;
+    const bool wide = mean_len * 1.1 > (double)KH_RAW_BYTES / 256.0 - 1.0;
     if (wide) {
         const uint64_t blocks = (m + 63) / 64;
         hipLaunchKernelGGL(k_key_hash<64>, dim3((uint32_t)blocks), dim3(64), 0, (hipStream_t)stream, bytes, nbytes,
-                           offsets, (uint64_t)m, seed, pre, key_id);
+                           offsets, (uint64_t)m, seed, cfg, pre, key_id);
     } else {
         const uint64_t blocks = (m + 255) / 256;
         hipLaunchKernelGGL(k_key_hash<256>, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, bytes, nbytes,
-                           offsets, (uint64_t)m, seed, pre, key_id);
+                           offsets, (uint64_t)m, seed, cfg, pre, key_id);
     }
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+extern "C" int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
+                                   uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id,
+                                   void* stream) {
+    return rl_hash_keys_launch(m, bytes, nbytes, offsets, seed, nullptr, prefix, prefix_len,
+                               m ? (double)nbytes / (double)m : 0.0, key_id, stream);
 }
 
 extern "C" int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,

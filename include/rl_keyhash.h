@@ -41,6 +41,16 @@ extern "C" {
 #endif
 
 #define RL_KEYHASH_MAX_PREFIX 240
+/* largest m per call: the launch grid is a 32-bit work-item count */
+#define RL_KEYHASH_MAX_KEYS ((uint64_t)0xFFFFFF00u)
+
+/* The seed the engine's raw-key entry point hashes request i with: the
+ * caller's seed with the request's config id mixed in, so each registered
+ * config is its own key namespace (config 0 keeps the seed).  Two configs
+ * never share state for one raw key -- a limiter instance owns its keys
+ * (DESIGN.md §1). */
+#define RL_CFG_SEED(seed, cfg_id) ((uint64_t)(seed) ^ ((uint64_t)(uint32_t)(cfg_id) * 0x9E3779B97F4A7C15ull))
+static inline uint64_t rl_cfg_seed(uint64_t seed, uint32_t cfg_id) { return RL_CFG_SEED(seed, cfg_id); }
 
 /* Device arrays, enqueued on `stream` (a hipStream_t; NULL = the null stream).
  * bytes: nbytes readable bytes; offsets: m + 1 entries. */
@@ -56,7 +66,8 @@ int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes
  * ids: the hashing above runs on the engine's grouping stream ahead of the
  * table probe, so batches stay pipelined (RL_OPT_PIPELINE).  key_bytes /
  * key_offsets are device arrays under the same completeness rule as the other
- * inputs; offsets are absolute into key_bytes (m + 1 entries). */
+ * inputs; offsets are absolute into key_bytes (m + 1 entries).  Request i's id
+ * is XXH64(FormatKey(prefix, key_i), rl_cfg_seed(seed, cfg_id[i])). */
 int rl_decide_batch_keys_device(rl_engine* e, size_t m, const uint8_t* key_bytes, uint64_t nbytes,
                                 const uint64_t* key_offsets, uint64_t seed, const char* prefix, size_t prefix_len,
                                 const int64_t* ts_ns, const int64_t* n, const uint32_t* cfg_id,

@@ -80,6 +80,12 @@ def key_id(prefix: bytes, key: bytes, seed: int) -> int:
     return KEY_RESERVED - 1 if h == KEY_RESERVED else h
 
 
+def cfg_seed(seed: int, cfg_id: int) -> int:
+    """rl_cfg_seed (include/rl_keyhash.h): the seed the engine's raw-key entry
+    point hashes a request of config `cfg_id` with."""
+    return (seed ^ ((cfg_id * 0x9E3779B97F4A7C15) & M64)) & M64
+
+
 def key_ids_fast(prefix: bytes, keys, seed: int):
     """Same as key_id over a list, through the xxhash package when importable
     (large GPU parity cases); falls back to the restatement."""

@@ -210,7 +210,10 @@ def test_gpu_decide_batch_keys_device(rl, pipeline):
         ts = t_last + np.cumsum(rng.integers(0, 200_000, m)).astype(np.int64)
         t_last = int(ts[-1])
         n = rng.choice([1, 1, 1, 3], m).astype(np.int64)
-        cfg = (pick % 3).astype(np.uint32)
+        # configs drawn independently of the key: one raw key is used under
+        # several configs (two window configs with different W included), each
+        # its own namespace (rl_cfg_seed)
+        cfg = rng.integers(0, 3, m).astype(np.uint32)
         d = [torch.from_numpy(x).to(dev) for x in (data, off.view(np.int64), ts, n, cfg.view(np.int32))]
         o = [torch.empty(m, dtype=torch.uint8, device=dev)] + \
             [torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)] + \
