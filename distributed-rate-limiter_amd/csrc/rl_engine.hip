@@ -49,7 +49,7 @@ __global__ void k_init_win(WinEntry* t, uint64_t n) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         t[i].key = EMPTY_KEY;
-        t[i].pad = 0;
+        t[i].nspill = 0;
         for (int k = 0; k < 2; k++) { t[i].s[k].ws = 0; t[i].s[k].cnt = 0; t[i].s[k].when = ABSENT; }
     }
 }
@@ -127,8 +127,8 @@ constexpr uint32_t SMALL_MAX = 4096;
 
 __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
     uint32_t m, ReqArgs in, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb, uint64_t tb_mask,
-    WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key, int32_t profile, ReqArgs ps,
-    TbPre pre, uint32_t heavy_min, uint32_t* eflags) {
+    WinEntry* win, uint64_t win_mask, Spill spill, uint32_t win_base, uint32_t invalid_key, int32_t profile,
+    ReqArgs ps, TbPre pre, uint32_t heavy_min, uint32_t* eflags) {
     __shared__ uint64_t sk[SMALL_MAX];   // (slot << 32) | arrival index
     __shared__ uint64_t heavy[SMALL_MAX / 32];   // (end << 32) | start of each long segment
     __shared__ uint32_t nheavy;
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
             continue;
         }
         if (k0 < win_base) replay_tb_serial(&tb[k0], j, j1, cfgs, profile, ps, pre);
-        else replay_win_serial(&win[k0 - win_base], j, j1, cfgs, profile, ps, eflags);
+        else replay_win_serial(&win[k0 - win_base], spill, j, j1, cfgs, profile, ps, eflags);
     }
     __syncthreads();
     {
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
             const uint32_t j0 = (uint32_t)heavy[h], j1 = (uint32_t)(heavy[h] >> 32);
             const uint32_t k0 = (uint32_t)(sk[j0] >> 32);
             if (k0 < win_base) wave_segment(&tb[k0], j0, j1, cfgs, profile, ps, pre, eflags, iters);
-            else wave_win_segment(&win[k0 - win_base], j0, j1, cfgs, profile, ps, eflags);
+            else wave_win_segment(&win[k0 - win_base], spill, j0, j1, cfgs, profile, ps, eflags);
         }
     }
     __syncthreads();
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
 // Reset: DEL of the key(s) AllowN would touch at ts (tokenbucket.go:136-144,
 // slidingwindow.go:125-139, fixedwindow.go:118-128)
 __global__ void k_reset(uint64_t key, int64_t ts, const CfgDev* cfgs, uint32_t cfg, TbEntry* tb,
-                        uint64_t tb_mask, WinEntry* win, uint64_t win_mask) {
+                        uint64_t tb_mask, WinEntry* win, uint64_t win_mask, Spill spill) {
     const CfgDev& c = cfgs[cfg];
     if (c.alg == ALG_TOKEN_BUCKET) {
         uint32_t s = probe_find(tb, tb_mask, key);
@@ -267,13 +267,9 @@ __global__ void k_reset(uint64_t key, int64_t ts, const CfgDev* cfgs, uint32_t c
     }
     uint32_t s = probe_find(win, win_mask, key);
     if (s == NO_SLOT) return;
-    int64_t ws = window_start(ts, c);
-    int64_t pws = ws - c.ttl_c;
-    for (int k = 0; k < 2; k++) {
-        if (win[s].s[k].when == ABSENT) continue;
-        if (win[s].s[k].ws == ws || (c.alg == ALG_SLIDING_WINDOW && win[s].s[k].ws == pws))
-            win[s].s[k].when = ABSENT;
-    }
+    const int64_t ws = window_start(ts, c);
+    wk_delete(&win[s], spill, ws);
+    if (c.alg == ALG_SLIDING_WINDOW) wk_delete(&win[s], spill, ws - c.ttl_c);
 }
 
 // diagnostic timestamp (10 ns ticks) into *w
@@ -370,6 +366,10 @@ struct rl_engine {
     uint64_t tb_cap = 0;
     WinEntry* d_win = nullptr;
     uint64_t win_cap = 0;
+    SpillEntry* d_spill = nullptr;    // window keys outside their user key's entry (rl_window.h)
+    uint64_t spill_cap = 0;
+    bool spill_follows = true;        // spill capacity = 2 x window capacity (also after a resize)
+    Spill spill() const { return Spill{d_spill, spill_cap - 1}; }
     uint32_t win_base = 0, invalid_key = 0;
     int sort_bits = 0, sort_passes = 0;
 
@@ -494,6 +494,7 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_cfg);
     (void)hipFree(e->d_tb);
     (void)hipFree(e->d_win);
+    (void)hipFree(e->d_spill);
     for (auto& B : e->set) free_set(B);
     (void)hipFree(e->d_eflags);
     (void)hipFree(e->small_kid);
@@ -538,6 +539,9 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     e->tb_cap = pow2_at_least(std::max<uint64_t>(o->tb_capacity, 1024));
     e->win_cap = pow2_at_least(std::max<uint64_t>(o->win_capacity, 1024));
     if (e->tb_cap + e->win_cap >= (1ull << 31)) { delete e; return RL_EINVAL; }
+    e->spill_follows = o->spill_capacity == 0;
+    e->spill_cap = pow2_at_least(std::max<uint64_t>(o->spill_capacity ? o->spill_capacity : 2 * e->win_cap, 1024));
+    if (e->spill_cap > (1ull << 34)) { delete e; return RL_EINVAL; }
     e->win_base = (uint32_t)e->tb_cap;
     e->invalid_key = (uint32_t)(e->tb_cap + e->win_cap);
     e->sort_bits = bitlen(e->invalid_key);
@@ -581,6 +585,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_cfg, sizeof(CfgDev) * e->cfg_cap) == hipSuccess;
     ok &= hipMalloc(&e->d_tb, sizeof(TbEntry) * e->tb_cap) == hipSuccess;
     ok &= hipMalloc(&e->d_win, sizeof(WinEntry) * e->win_cap) == hipSuccess;
+    ok &= hipMalloc(&e->d_spill, sizeof(SpillEntry) * e->spill_cap) == hipSuccess;
     for (auto& B : e->set) ok = ok && alloc_set(B, M, e->zero_bytes, status_words);
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
     ok &= hipMalloc(&e->d_key, 8 * M) == hipSuccess;
@@ -602,6 +607,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (!ok) return bail(RL_ENOMEM);
     k_init_tb<<<2048, 256, 0, e->stream>>>(e->d_tb, e->tb_cap);
     k_init_win<<<2048, 256, 0, e->stream>>>(e->d_win, e->win_cap);
+    k_init_spill<<<2048, 256, 0, e->stream>>>(e->d_spill, e->spill_cap);
     if (hipMemsetAsync(e->d_eflags, 0, 4, e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (hipStreamSynchronize(e->stream) != hipSuccess) return bail(RL_EDEVICE);
     if (hipDeviceSynchronize() != hipSuccess) return bail(RL_EDEVICE);
@@ -718,7 +724,7 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, e->s_sms, e->s_dec, e->s_rem, e->s_retry, e->s_reset, e->s_tok};
     TbPre pre{e->s_add, e->s_th, e->s_reset, e->s_lq, e->s_when};
     k_small<<<1, SMALL_BLOCK, 0, c>>>(m, a, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
-                                      e->win_cap - 1, e->win_base, e->invalid_key, e->profile, ps, pre,
+                                      e->win_cap - 1, e->spill(), e->win_base, e->invalid_key, e->profile, ps, pre,
                                       std::max<uint32_t>(e->heavy_min, 32), e->d_eflags);
     HIPCHK(e, hipEventRecord(e->ev_small, c));
     HIPCHK(e, hipStreamWaitEvent(s, e->ev_small, 0));
@@ -802,11 +808,11 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
     if (ncfg <= (uint32_t)MAX_LCFG)
-        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, e->chain_pad[0], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
+        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, e->chain_pad[0], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(),
                                                            e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
                                                            B.runs);
     else
-        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, e->chain_pad[1], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win,
+        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, e->chain_pad[1], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(),
                                                             e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
                                                             B.runs);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 19);
@@ -956,7 +962,7 @@ extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t 
     int r = drain(e);
     if (r != RL_OK) return r;
     k_reset<<<1, 1, 0, e->stream>>>(key_id, ts_ns, e->d_cfg, cfg_id, e->d_tb, e->tb_cap - 1, e->d_win,
-                                     e->win_cap - 1);
+                                     e->win_cap - 1, e->spill());
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return RL_OK;
@@ -968,17 +974,18 @@ extern "C" int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* ou
     int r = drain(e);
     if (r != RL_OK) return r;
     unsigned long long* d = nullptr;
-    HIPCHK(e, hipMalloc(&d, 4 * sizeof(unsigned long long)));
-    unsigned long long h[4] = {0, 0, 0, 0};
+    HIPCHK(e, hipMalloc(&d, 6 * sizeof(unsigned long long)));
+    unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
     hipStream_t s = e->stream;
     bool ok = hipMemsetAsync(d, 0, sizeof h, s) == hipSuccess;
     k_table_count<<<1024, 256, 0, s>>>(e->d_tb, e->tb_cap, now_ms, e->profile, d);
     k_table_count<<<1024, 256, 0, s>>>(e->d_win, e->win_cap, now_ms, e->profile, d + 2);
+    k_table_count<<<1024, 256, 0, s>>>(e->d_spill, e->spill_cap, now_ms, e->profile, d + 4);
     ok = ok && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipStreamSynchronize(s) == hipSuccess;
     (void)hipFree(d);
     if (!ok) return fail(e, RL_EDEVICE, "table count failed");
-    *out = rl_table_info{e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3]};
+    *out = rl_table_info{e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3], e->spill_cap, h[4], h[5]};
     return RL_OK;
 }
 
@@ -988,50 +995,60 @@ extern "C" int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, u
     (void)hipSetDevice(e->device);
     const uint64_t tb_cap = tb_capacity ? pow2_at_least(std::max<uint64_t>(tb_capacity, 1024)) : e->tb_cap;
     const uint64_t win_cap = win_capacity ? pow2_at_least(std::max<uint64_t>(win_capacity, 1024)) : e->win_cap;
+    const uint64_t spill_cap = e->spill_follows ? pow2_at_least(std::max<uint64_t>(2 * win_cap, 1024)) : e->spill_cap;
     if (tb_cap + win_cap >= (1ull << 31)) return fail(e, RL_EINVAL, "table capacities too large");
     int r = drain(e);
     if (r != RL_OK) return r;
     TbEntry* ntb = nullptr;
     WinEntry* nwin = nullptr;
+    SpillEntry* nsp = nullptr;
     unsigned long long* d = nullptr;
     bool ok = hipMalloc(&ntb, sizeof(TbEntry) * tb_cap) == hipSuccess;
     ok = ok && hipMalloc(&nwin, sizeof(WinEntry) * win_cap) == hipSuccess;
-    ok = ok && hipMalloc(&d, 4 * sizeof(unsigned long long)) == hipSuccess;
+    ok = ok && hipMalloc(&nsp, sizeof(SpillEntry) * spill_cap) == hipSuccess;
+    ok = ok && hipMalloc(&d, 6 * sizeof(unsigned long long)) == hipSuccess;
     if (!ok) {
-        (void)hipFree(ntb); (void)hipFree(nwin); (void)hipFree(d);
+        (void)hipFree(ntb); (void)hipFree(nwin); (void)hipFree(nsp); (void)hipFree(d);
         return fail(e, RL_ENOMEM, "table gc: allocation failed");
     }
-    unsigned long long h[4] = {0, 0, 0, 0};
+    unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
     hipStream_t s = e->stream;
     k_init_tb<<<2048, 256, 0, s>>>(ntb, tb_cap);
     k_init_win<<<2048, 256, 0, s>>>(nwin, win_cap);
+    k_init_spill<<<2048, 256, 0, s>>>(nsp, spill_cap);
     ok = hipMemsetAsync(d, 0, sizeof h, s) == hipSuccess;
     k_rehash<<<2048, 256, 0, s>>>(e->d_tb, e->tb_cap, ntb, tb_cap - 1, now_ms, e->profile, d);
     k_rehash<<<2048, 256, 0, s>>>(e->d_win, e->win_cap, nwin, win_cap - 1, now_ms, e->profile, d + 2);
+    // after the window entries: each live spill entry is counted in its new entry
+    k_spill_rehash<<<2048, 256, 0, s>>>(e->d_spill, e->spill_cap, nsp, spill_cap - 1, nwin, win_cap - 1, now_ms,
+                                        e->profile, d + 4);
     ok = ok && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipStreamSynchronize(s) == hipSuccess;
     (void)hipFree(d);
-    if (!ok || h[1] || h[3]) {
+    if (!ok || h[1] || h[3] || h[5]) {
         (void)hipFree(ntb);
         (void)hipFree(nwin);
+        (void)hipFree(nsp);
         return ok ? fail(e, RL_ENOMEM, "table gc: live keys do not fit the requested capacity")
                   : fail(e, RL_EDEVICE, "table gc failed");
     }
     (void)hipFree(e->d_tb);
     (void)hipFree(e->d_win);
+    (void)hipFree(e->d_spill);
     e->d_tb = ntb;
     e->d_win = nwin;
+    e->d_spill = nsp;
     // slot ids (the sort keys) follow the capacities
     e->tb_cap = tb_cap;
     e->win_cap = win_cap;
+    e->spill_cap = spill_cap;
     e->win_base = (uint32_t)tb_cap;
     e->invalid_key = (uint32_t)(tb_cap + win_cap);
     e->sort_bits = bitlen(e->invalid_key);
     e->sort_passes = (e->sort_bits + 7) / 8;
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
-    if (out) *out = rl_table_info{tb_cap, h[0], h[0], win_cap, h[2], h[2]};
-    return RL_OK;
+    return out ? rl_table_info_get(e, now_ms, out) : RL_OK;
 }
 
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {

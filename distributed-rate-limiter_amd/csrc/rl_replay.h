@@ -12,6 +12,7 @@
 
 #include "rl_semantics.h"
 #include "rl_table.h"
+#include "rl_window.h"
 
 namespace rl {
 
@@ -146,24 +147,28 @@ __device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, co
     e->when = pre.when[j1 - 1];
 }
 
-__device__ inline void replay_win_serial(WinEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
-                                         int32_t profile, const ReqArgs& a, uint32_t* eflags) {
-    WinState w;
-    w.s[0] = e->s[0];
-    w.s[1] = e->s[1];
-    uint32_t ef = 0;
+// requests [j0, j1) of one window segment, one by one, from state w
+__device__ inline void replay_win_steps(WinState& w, const Spill& S, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
+                                        int32_t profile, const ReqArgs& a, uint32_t& ef) {
+    if (j0 >= j1) return;
     Req cur = load_req(a, j0);
     for (uint32_t j = j0; j < j1; j++) {
         Req nxt = cur;
         if (j + 1 < j1) nxt = load_req(a, j + 1);
         const CfgDev& c = cfgs[cur.c];
-        Out o = (c.alg == ALG_SLIDING_WINDOW) ? sw_step(w, cur.t, cur.n, cur.sms, c, profile, ef)
-                                              : fw_step(w, cur.t, cur.n, cur.sms, c, profile, ef);
+        Out o = (c.alg == ALG_SLIDING_WINDOW) ? sw_step(w, S, cur.t, cur.n, cur.sms, c, profile, ef)
+                                              : fw_step(w, S, cur.t, cur.n, cur.sms, c, profile, ef);
         write_out(a, j, o);
         cur = nxt;
     }
-    e->s[0] = w.s[0];
-    e->s[1] = w.s[1];
+}
+
+__device__ inline void replay_win_serial(WinEntry* e, const Spill& S, uint32_t j0, uint32_t j1,
+                                         const CfgDev* cfgs, int32_t profile, const ReqArgs& a, uint32_t* eflags) {
+    WinState w = win_load(e);
+    uint32_t ef = 0;
+    replay_win_steps(w, S, j0, j1, cfgs, profile, a, ef);
+    win_store(e, w);
     if (ef) atomicOr(eflags, ef);
 }
 

@@ -28,7 +28,7 @@ enum : int32_t { PROFILE_REDIS7 = 0, PROFILE_MINIREDIS = 1 };
 // error-flag bits raised by kernels (sticky per engine)
 enum : uint32_t {
     EF_TABLE_FULL = 1u,       // open-addressing table has no free slot
-    EF_ORDER = 2u,            // a live window key was evicted (per-key time went backwards)
+    EF_ORDER = 2u,            // reserved (no longer raised: window keys spill, rl_window.h)
     EF_LOOKBACK = 4u,         // radix-sort look-back spin bound hit
     EF_BAD_KEY = 8u,          // key id equal to the reserved empty marker
     EF_INTERNAL = 16u,        // cooperative replay invariant violated (never expected)
@@ -184,41 +184,15 @@ RL_HD inline Out tb_step(TbState& st, int64_t t, int64_t n, int64_t s_ms, const 
 }
 
 // ---------------------------------------------------------------------------
-// Window counters.  A user key's window keys "B:ws" live in a 2-slot mini
-// keyspace: under per-key non-decreasing time only the two most recent window
-// keys can ever be read again.
+// Window counters: one Redis string key "B:ws" per (user key, window start)
+// (fixedwindow.go:75, slidingwindow.go:78-79).  The keyspace holding them is
+// in rl_window.h (a 2-slot entry per user key + a spill table).
 // ---------------------------------------------------------------------------
 struct WinSlot {
     int64_t ws;
     int64_t cnt;
     int64_t when;
 };
-struct WinState {
-    WinSlot s[2];
-};
-
-// lookupKey with lazy expiry; returns slot index or -1
-RL_HD inline int win_find(WinState& w, int64_t ws, int64_t s_ms, int32_t profile) {
-    for (int k = 0; k < 2; k++) {
-        if (w.s[k].when == ABSENT || w.s[k].ws != ws) continue;
-        if (!key_alive(w.s[k].when, s_ms, profile)) { w.s[k].when = ABSENT; continue; }
-        return k;
-    }
-    return -1;
-}
-
-// slot for a key that INCRBY is about to create; `keep` (or -1) must survive
-RL_HD inline int win_alloc(WinState& w, int keep, int64_t ws, int64_t s_ms, int32_t profile,
-                           uint32_t& eflags) {
-    int best = -1;
-    for (int k = 0; k < 2; k++) {
-        if (k == keep) continue;
-        if (!key_alive(w.s[k].when, s_ms, profile)) return k;       // free or expired
-        if (best < 0 || w.s[k].ws < w.s[best].ws) best = k;
-    }
-    if (w.s[best].ws > ws) eflags |= EF_ORDER;                      // evicting a newer live key
-    return best;
-}
 
 RL_HD inline int64_t until_reset(int64_t reset_at, int64_t t) {
     int64_t d = wsub(reset_at, t);
@@ -228,79 +202,6 @@ RL_HD inline int64_t until_reset(int64_t reset_at, int64_t t) {
 // INCRBY overflow rule (t_string.c incrDecrCommand)
 RL_HD inline bool incr_overflows(int64_t old, int64_t n) {
     return (n < 0 && old < 0 && n < (INT64_MIN - old)) || (n > 0 && old > 0 && n > (INT64_MAX - old));
-}
-
-// fixedWindowScript (fixedwindow.go:21-27) + AllowN (fixedwindow.go:65-115)
-RL_HD inline Out fw_step(WinState& w, int64_t t, int64_t n, int64_t s_ms, const CfgDev& c,
-                         int32_t profile, uint32_t& eflags) {
-    Out o;
-    o.tokens = 0.0;
-    int64_t ws = window_start(t, c);
-    o.reset_at = wadd(wmul(ws, NS_PER_S), c.window);
-    int k = win_find(w, ws, s_ms, profile);
-    int64_t old = k >= 0 ? w.s[k].cnt : 0;
-    if (incr_overflows(old, n)) {
-        o.decision = DEC_ERROR; o.remaining = 0; o.retry = 0;
-        return o;
-    }
-    if (k < 0) {
-        k = win_alloc(w, -1, ws, s_ms, profile, eflags);
-        w.s[k].ws = ws; w.s[k].cnt = 0; w.s[k].when = NO_EXPIRY;
-    }
-    int64_t cur = old + n;
-    w.s[k].cnt = cur;
-    if ((double)cur == (double)n) w.s[k].when = expire_when(c.ttl_c, s_ms);
-    int64_t count = go_f2i((double)cur);
-    bool allowed = count <= c.limit;
-    int64_t rem = wsub(c.limit, count);
-    o.remaining = rem < 0 ? 0 : rem;
-    o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
-    o.retry = allowed ? 0 : until_reset(o.reset_at, t);
-    return o;
-}
-
-// slidingWindowScript (slidingwindow.go:22-30) + AllowN (slidingwindow.go:68-122)
-RL_HD inline Out sw_step(WinState& w, int64_t t, int64_t n, int64_t s_ms, const CfgDev& c,
-                         int32_t profile, uint32_t& eflags) {
-    Out o;
-    o.tokens = 0.0;
-    int64_t ws = window_start(t, c);
-    int64_t pws = ws - c.ttl_c;
-    o.reset_at = wadd(wmul(ws, NS_PER_S), c.window);
-    // local prev = tonumber(redis.call('GET', KEYS[2]) or 0)
-    int pk = win_find(w, pws, s_ms, profile);
-    double prev = pk >= 0 ? (double)w.s[pk].cnt : 0.0;
-    // local curr = redis.call('INCRBY', KEYS[1], ARGV[1])
-    int ck = win_find(w, ws, s_ms, profile);
-    int64_t old = ck >= 0 ? w.s[ck].cnt : 0;
-    if (incr_overflows(old, n)) {
-        o.decision = DEC_ERROR; o.remaining = 0; o.retry = 0;
-        return o;
-    }
-    if (ck < 0) {
-        ck = win_alloc(w, pk, ws, s_ms, profile, eflags);
-        w.s[ck].ws = ws; w.s[ck].cnt = 0; w.s[ck].when = NO_EXPIRY;
-    }
-    int64_t cur = old + n;
-    w.s[ck].cnt = cur;
-    // if curr == tonumber(ARGV[1]) then EXPIRE KEYS[1] ARGV[2]
-    if ((double)cur == (double)n) w.s[ck].when = expire_when(c.ttl_c, s_ms);
-    // EXPIRE KEYS[2] ARGV[3]  (no-op when the key does not exist)
-    pk = win_find(w, pws, s_ms, profile);
-    if (pk >= 0) w.s[pk].when = expire_when(c.ttl_p, s_ms);
-    int64_t p = go_f2i(prev);
-    int64_t cc = go_f2i((double)cur);
-    // calculateWeightedCount (slidingwindow.go:190-197)
-    int64_t elapsed = wsub(t, wmul(ws, NS_PER_S));
-    double progress = (double)elapsed / (double)c.window;
-    double weighted = (double)p * (1.0 - progress);
-    weighted = weighted + (double)cc;
-    bool allowed = weighted <= c.limit_d;
-    int64_t rem = wsub(c.limit, go_f2i(weighted));
-    o.remaining = rem < 0 ? 0 : rem;
-    o.decision = allowed ? DEC_ALLOWED : DEC_DENIED;
-    o.retry = allowed ? 0 : until_reset(o.reset_at, t);
-    return o;
 }
 
 }  // namespace rl

@@ -27,10 +27,31 @@ static_assert(sizeof(TbEntry) == 32, "TbEntry must be 32 bytes");
 
 struct alignas(64) WinEntry {
     uint64_t key;
-    int64_t pad;
+    int64_t nspill;  // this user key's entries in the spill table (rl_window.h)
     WinSlot s[2];
 };
 static_assert(sizeof(WinEntry) == 64, "WinEntry must be 64 bytes");
+
+// The rest of the window keyspace.  Redis keeps any number of live window
+// keys "B:ws" per user key B (fixedwindow.go:72-75, slidingwindow.go:74-79);
+// the 2-slot entry holds the two newest, and a live key that has to leave it
+// (or an older window key created out of order) lives here.  Open addressing
+// by the USER key with linear probing from spill_home(k): every spill entry
+// of k sits before the first never-used slot of k's probe sequence (key ids
+// are never removed), and only k's segment -- one thread or one wave of one
+// replay -- touches them, so k reuses its own dead entries without races.
+struct alignas(32) SpillEntry {
+    uint64_t key;    // user key id (EMPTY_KEY: never used)
+    int64_t ws;      // window start (Unix s)
+    int64_t cnt;
+    int64_t when;    // expiry (server ms); ABSENT: deleted (the slot stays k's)
+};
+static_assert(sizeof(SpillEntry) == 32, "SpillEntry must be 32 bytes");
+
+struct Spill {
+    SpillEntry* tab;
+    uint64_t mask;
+};
 
 RL_HD inline uint64_t mix64(uint64_t x) {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
@@ -88,6 +109,24 @@ __device__ inline bool entry_live(const WinEntry& x, int64_t now_ms, int32_t pro
         if (x.s[k].when != ABSENT && key_alive(x.s[k].when, now_ms, profile)) return true;
     return false;
 }
+__device__ inline bool entry_live(const SpillEntry& x, int64_t now_ms, int32_t profile) {
+    return x.key != EMPTY_KEY && x.when != ABSENT && key_alive(x.when, now_ms, profile);
+}
+
+// what table GC keeps: a window entry also stays while its user key has
+// spill entries (their liveness is recounted by k_spill_rehash)
+__device__ inline bool entry_kept(const TbEntry& x, int64_t now_ms, int32_t profile) {
+    return entry_live(x, now_ms, profile);
+}
+__device__ inline bool entry_kept(const WinEntry& x, int64_t now_ms, int32_t profile) {
+    return x.key != EMPTY_KEY && (x.nspill > 0 || entry_live(x, now_ms, profile));
+}
+__device__ inline void gc_copy(TbEntry& dst, const TbEntry& x) { dst = x; }
+__device__ inline void gc_copy(WinEntry& dst, const WinEntry& x) {
+    WinEntry y = x;
+    y.nspill = 0;   // recounted from the live spill entries
+    dst = y;
+}
 
 // Table GC / resize (rl_table_gc): re-insert every live entry of `old` into
 // the empty table `nu`.  Keys are distinct, so concurrent inserts never race
@@ -100,14 +139,55 @@ __global__ void k_rehash(const E* __restrict__ old, uint64_t n_old, E* nu, uint6
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_old;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const E x = old[i];
-        if (!entry_live(x, now_ms, profile)) continue;
+        if (!entry_kept(x, now_ms, profile)) continue;
         live++;
         const uint32_t s = probe_insert(nu, mask_new, x.key);
         if (s == NO_SLOT) { lost++; continue; }
-        nu[s] = x;
+        gc_copy(nu[s], x);
     }
     if (live) atomicAdd(&counters[0], live);
     if (lost) atomicAdd(&counters[1], lost);
+}
+
+__device__ inline uint64_t spill_home(uint64_t k, uint64_t mask) { return mix64(k ^ 0x5bd1e9955bd1e995ULL) & mask; }
+
+// Table GC of the spill table, after the window table's k_rehash: every live
+// spill entry moves to the fresh spill table (strict CAS: two entries of one
+// user key may be moved at once) and is counted in its user key's new window
+// entry.  counters as k_rehash.
+__global__ void k_spill_rehash(const SpillEntry* __restrict__ old, uint64_t n_old, SpillEntry* nu, uint64_t mask_new,
+                               WinEntry* win, uint64_t win_mask, int64_t now_ms, int32_t profile,
+                               unsigned long long* counters) {
+    unsigned long long live = 0, lost = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_old;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const SpillEntry x = old[i];
+        if (!entry_live(x, now_ms, profile)) continue;
+        live++;
+        const uint32_t w = probe_find(win, win_mask, x.key);
+        uint64_t h = spill_home(x.key, mask_new);
+        bool placed = false;
+        for (uint64_t p = 0; w != NO_SLOT && p <= mask_new && p < MAX_PROBES; p++) {
+            if (atomicCAS((unsigned long long*)&nu[h].key, (unsigned long long)EMPTY_KEY,
+                          (unsigned long long)x.key) == EMPTY_KEY) {
+                nu[h].ws = x.ws;
+                nu[h].cnt = x.cnt;
+                nu[h].when = x.when;
+                atomicAdd((unsigned long long*)&win[w].nspill, 1ull);
+                placed = true;
+                break;
+            }
+            h = (h + 1) & mask_new;
+        }
+        if (!placed) lost++;
+    }
+    if (live) atomicAdd(&counters[0], live);
+    if (lost) atomicAdd(&counters[1], lost);
+}
+
+__global__ void k_init_spill(SpillEntry* t, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        t[i] = SpillEntry{EMPTY_KEY, 0, 0, ABSENT};
 }
 
 // occupied and live entries (rl_table_info_get)

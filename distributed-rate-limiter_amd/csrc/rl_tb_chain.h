@@ -798,10 +798,13 @@ __device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, u
 // expiry, slot allocation), the rest are computed in parallel from a prefix
 // sum of n and checked request by request against every assumption of that
 // shortcut -- the current key alive, no INCRBY overflow, no TTL reset,
-// the previous key's refresh chain -- and any failed check (or a mixed-config
-// segment, or sub-second windows) replays the segment serially instead.
-__device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry* e, uint32_t j0, uint32_t j1,
-                                                                      const CfgDev* __restrict__ cfgs,
+// the previous key's refresh chain.  A failed check (or a config change, a
+// key in the spill, sub-second windows) continues serially from the first
+// request not yet applied, on the exact state reached so far: the first
+// request of a run has side effects on the spill table, so nothing is ever
+// replayed twice.
+__device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry* e, const Spill& S, uint32_t j0,
+                                                                      uint32_t j1, const CfgDev* __restrict__ cfgs,
                                                                       int32_t profile, const ReqArgs& a,
                                                                       uint32_t* eflags) {
     constexpr int K = CH_K;
@@ -809,18 +812,16 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
     const uint32_t c0 = a.cfg[j0];
     const CfgDev& C = cfgs[c0];
     const bool sw = C.alg == ALG_SLIDING_WINDOW;
-    WinState w;
-    w.s[0] = e->s[0];
-    w.s[1] = e->s[1];
+    WinState w = win_load(e);
     uint32_t ef = 0;
     bool ok = C.ttl_c > 0;
     uint32_t pos = j0;
     while (ok && pos < j1) {
         // first request of the run: exact
         const Req r0 = load_req(a, pos);
-        if (r0.c != c0) { ok = false; break; }
-        const Out o0 = sw ? sw_step(w, r0.t, r0.n, r0.sms, C, profile, ef)
-                          : fw_step(w, r0.t, r0.n, r0.sms, C, profile, ef);
+        if (r0.c != c0) { ok = false; break; }   // serial from pos
+        const Out o0 = sw ? sw_step(w, S, r0.t, r0.n, r0.sms, C, profile, ef)
+                          : fw_step(w, S, r0.t, r0.n, r0.sms, C, profile, ef);
         if (lane == 0) write_out(a, pos, o0);
         const int64_t ws = window_start(r0.t, C), pws = ws - C.ttl_c;
         int ck = -1, pk = -1;
@@ -829,12 +830,15 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
             if (w.s[k].ws == ws) ck = k;
             else if (sw && w.s[k].ws == pws) pk = k;
         }
+        pos++;   // r0 is applied
         if (o0.decision == DEC_ERROR || ck < 0) { ok = false; break; }
+        // the run's shortcut keeps the previous window's key in the entry; one
+        // in the spill (per-key time went back) takes the serial path
+        if (sw && pk < 0 && spill_lookup(S, w.key, w.nspill, pws)) { ok = false; break; }
         const int64_t when_c = w.s[ck].when;
         const int64_t cnt_p = pk >= 0 ? w.s[pk].cnt : 0;
         int64_t c_run = w.s[ck].cnt, sms_prev = r0.sms;
         bool p_alive = pk >= 0;
-        pos++;
         bool run_end = false;
         while (ok && !run_end && pos < j1) {
             // K requests per lane; the run ends at the first other window / config
@@ -855,6 +859,7 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
             const uint32_t cend = wave_min_u32(firstx);            // run end in this chunk (relative)
             const uint32_t lim = min(min(cend, j1 - pos), (uint32_t)(64 * K));
             run_end = cend != NO_STOP;
+            if (lim == 0) break;   // the run was r0 alone: nothing to carry
             // prefix sum of n (int64) inside the run, per-request checks
             int64_t ls = 0;
 #pragma unroll
@@ -880,7 +885,7 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
                 sp = sm[q];
                 c = cur;
             }
-            if (__ballot(bad)) { ok = false; break; }
+            if (__ballot(bad)) { ok = false; break; }   // serial from pos (this chunk)
             const uint32_t pd = wave_min_u32(pdead_at);             // first request that finds prev dead
             // outputs
             c = c_run + li - ls;
@@ -923,19 +928,13 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
             if (pd != NO_STOP) p_alive = false;
             pos += lim;
         }
-        if (!ok) break;
-        // the state after the run
+        // the state after the run's applied requests
         w.s[ck].cnt = c_run;
         if (pk >= 0) w.s[pk].when = p_alive ? expire_when(C.ttl_p, sms_prev) : ABSENT;
     }
-    if (!ok) {
-        // replay the whole segment serially (outputs written so far are rewritten)
-        if (lane == 0) replay_win_serial(e, j0, j1, cfgs, profile, a, eflags);
-        return;
-    }
     if (lane == 0) {
-        e->s[0] = w.s[0];
-        e->s[1] = w.s[1];
+        if (!ok) replay_win_steps(w, S, pos, j1, cfgs, profile, a, ef);
+        win_store(e, w);
         if (ef) atomicOr(eflags, ef);
     }
 }
@@ -1146,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
 // hot keys' blocks stay in phase 1 while the others drain phases 2-3.
 template <bool LCFG>
 __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restrict__ sk, SegLists L, uint32_t* qctr,
-                                                       uint32_t win_base, TbEntry* tb, WinEntry* win,
+                                                       uint32_t win_base, TbEntry* tb, WinEntry* win, Spill spill,
                                                        const CfgDev* __restrict__ gcfgs, uint32_t ncfg,
                                                        int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
                                                        uint32_t* dbg, TbRuns runs) {
@@ -1211,7 +1210,7 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
                 wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
             } else {
                 const SegRec sg = L.list[2][u - nheavy];
-                wave_win_segment(&win[sk[sg.j0] - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+                wave_win_segment(&win[sk[sg.j0] - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
             }
         }
     }
@@ -1228,7 +1227,7 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
             const SegRec sg = L.list[1][u];
             const uint32_t k0 = sk[sg.j0];
             if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre);
-            else replay_win_serial(&win[k0 - win_base], sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+            else replay_win_serial(&win[k0 - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
         }
     }
     if (threadIdx.x == 0 && dbg) {

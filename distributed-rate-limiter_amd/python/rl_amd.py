@@ -44,6 +44,7 @@ class rl_opts(C.Structure):
         ("win_capacity", C.c_uint64),
         ("max_batch", C.c_uint32),
         ("flags", C.c_uint32),
+        ("spill_capacity", C.c_uint64),
     ]
 
 
@@ -74,7 +75,7 @@ class rll_result(C.Structure):
 
 class rl_table_info(C.Structure):
     _fields_ = [(k, C.c_uint64) for k in ("tb_capacity", "tb_used", "tb_live", "win_capacity", "win_used",
-                                          "win_live")]
+                                          "win_live", "spill_capacity", "spill_used", "spill_live")]
 
 
 class rl_coalescer_opts(C.Structure):
@@ -186,8 +187,8 @@ class Engine:
     """rl_engine: the batched decision engine on one GPU."""
 
     def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
-                 max_batch=1 << 20, device=0, flags=0):
-        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, flags)
+                 max_batch=1 << 20, device=0, flags=0, spill_capacity=0):
+        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, flags, spill_capacity)
         h = vp()
         rc = lib.rl_engine_create(C.byref(o), C.byref(h))
         if rc != RL_OK:
@@ -358,7 +359,7 @@ class LimiterEngine:
 
     def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
                  max_batch=1 << 16, device=0):
-        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, 0)
+        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, 0, 0)
         h = vp()
         buf = C.create_string_buffer(512)
         rc = lib.rll_engine_new(C.byref(o), C.byref(h), buf, 512)

@@ -33,7 +33,7 @@ extern "C" {
 #define RL_ENOMEM    (-12)  /* device allocation failed or state table full */
 #define RL_EDEVICE    (-5)  /* HIP runtime error (text in rl_last_error) */
 #define RL_ETIMEOUT (-110)  /* a device-side bounded wait expired */
-#define RL_EORDER    (-34)  /* per-key window ids went backwards (contract breach) */
+#define RL_EORDER    (-34)  /* reserved: no longer returned (window keys of any age are kept) */
 
 /* algorithms (interface.go:11-23) */
 #define RL_ALG_TOKEN_BUCKET   1
@@ -62,6 +62,9 @@ typedef struct rl_opts {
     uint64_t win_capacity;  /* window-counter table slots; rounded up to a power of 2 */
     uint32_t max_batch;     /* largest batch one launch sequence handles (<= 2^28) */
     uint32_t flags;         /* RL_OPT_* */
+    uint64_t spill_capacity; /* window keys kept outside their user key's table entry (a live key
+                                evicted by a newer window, or created out of order); rounded up to a
+                                power of 2; 0 = 2 x win_capacity (a sliding window key holds ~2) */
 } rl_opts;
 
 /* rl_opts.flags: the device-API input arrays of every rl_decide_batch_device
@@ -137,13 +140,15 @@ int rl_engine_stats(rl_engine* e, rl_stats* out);
 typedef struct rl_table_info {
     uint64_t tb_capacity, tb_used, tb_live;
     uint64_t win_capacity, win_used, win_live;
+    uint64_t spill_capacity, spill_used, spill_live;   /* spill slots ever claimed / live window keys */
 } rl_table_info;
 int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* out);
 
 /* Table GC (the TTLs of tokenbucket.go:170,
  * slidingwindow.go:161-162, fixedwindow.go:151): drop every key expired at
  * server clock now_ms -- Redis's active expiry -- and optionally resize the
- * tables (0 = keep the capacity).  Keys are only ever inserted by the decision
+ * tables (0 = keep the capacity; the spill table follows win_capacity when
+ * rl_opts.spill_capacity was 0, else keeps its capacity).  Keys are only ever inserted by the decision
  * path, so this is what keeps a long-running table from filling.  Decisions
  * are unchanged provided no later request carries a server clock below
  * now_ms (lazy expiry would see those keys as absent anyway).  Synchronous;

@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 import traces
-from tracegen import CONFIG_SETS, T0, NS, random_trace
+from tracegen import CONFIG_SETS, T0, NS, random_trace, skewed_trace
 
 pytestmark = pytest.mark.gpu
 
@@ -190,6 +190,51 @@ def test_config2_sw_bursty(rl):
 def test_config3_mixed(rl):
     g = traces.MixedTenants(nkeys=300_000, batch=500_000)
     run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 19, win=1 << 20)
+
+
+# --- per-key time going back (window keys beyond the 2-slot entry) -------------
+
+@pytest.mark.parametrize("profile", [0, 1])
+@pytest.mark.parametrize("kind", ["sw", "fw", "mixed"])
+@pytest.mark.parametrize("nkeys", [40, 3000])
+def test_skewed_clocks(rl, profile, kind, nkeys):
+    """App servers whose clocks differ by up to 130 s share the limiter: a
+    key's requests go back by one or more windows, so older live window keys
+    are spilled from the 2-slot entry and read back (rl_window.h).  Few keys:
+    heavy segments (wave replay); many keys: light ones; small batches: k_small.
+    The Redis clock is the store's own and monotone."""
+    configs = CONFIG_SETS[kind]
+    tr = skewed_trace(600 + profile * 7 + nkeys, 80_000, nkeys, configs, big_n=True)
+    run_both(rl, profile, configs, split(tr, [3000, 500, 20_000, 26_500, 30_000]), tb=1 << 14, win=1 << 14)
+
+
+def test_skewed_clocks_gc_and_reset(rl):
+    """Table GC (grow, then shrink) and Reset with spilled window keys."""
+    configs = CONFIG_SETS["mixed"]
+    tr = skewed_trace(640, 60_000, 500, configs)
+    eng = make_engine(rl, 0, tb=1 << 13, win=1 << 13, max_batch=1 << 15)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    caps = [(0, 0), (1 << 15, 1 << 15), (1 << 12, 1 << 12)]
+    for i, (key, ts, n, cfg, sms) in enumerate(split(tr, [15_000] * 4)):
+        if i:
+            now_ms = int(sms[0])
+            before = eng.table_info(now_ms)
+            _, after = eng.table_gc(now_ms, *caps[i - 1])
+            assert after.spill_live == before.spill_live
+            assert after.spill_used == after.spill_live <= before.spill_used
+        res = eng.decide(key, ts, n, cfg, sms)
+        assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
+        t, s_ms = int(ts[-1]), int(sms[-1])
+        for k in range(0, 500, 7):
+            # DEL of the keys AllowN would touch at a skewed server's time
+            for tt in (t, t - 7 * NS):
+                eng.reset(k % len(configs), k, tt)
+                sim.reset(k % len(configs), k, tt, s_ms)
+    assert eng.table_info(int(tr[4][-1])).spill_used > 0   # the spill was exercised
+    eng.close()
 
 
 # --- edges ----------------------------------------------------------------------

@@ -91,7 +91,7 @@ def test_lua_tostring_roundtrip(lib):
 
 # --- C oracle vs independent Python restatement --------------------------------
 
-from tracegen import CONFIG_SETS, random_trace  # noqa: E402
+from tracegen import CONFIG_SETS, random_trace, skewed_trace  # noqa: E402
 
 
 @pytest.mark.parametrize("profile", [0, 1])
@@ -113,6 +113,22 @@ def test_c_vs_python(lib, profile, kind, ff):
         assert got == d[:4], (i, got, d)
         if configs[cfg[i]][0] == 1 and d[0] in (0, 1):
             assert tok[i] == d[4] or (math.isnan(tok[i]) and math.isnan(d[4]))
+
+
+@pytest.mark.parametrize("profile", [0, 1])
+@pytest.mark.parametrize("kind", ["sw", "fw", "mixed"])
+def test_c_vs_python_skewed_clocks(lib, profile, kind):
+    # per-key times going back by one or more windows (skewed app servers)
+    configs = CONFIG_SETS[kind]
+    keys, ts, n, cfg, sms = skewed_trace(500 + profile, 3000, 30, configs, big_n=True)
+    c = oracle.OracleSim(profile)
+    p = P.Sim(profile)
+    for a, L, W in configs:
+        assert c.add_config(a, L, W) == p.add_config(a, L, W)
+    dec, rem, retry, reset, tok = c.decide(keys, ts, n, cfg, sms)
+    for i in range(len(keys)):
+        d = p.decide(int(keys[i]), int(ts[i]), int(n[i]), int(cfg[i]), int(sms[i]))
+        assert (int(dec[i]), int(rem[i]), int(retry[i]), int(reset[i])) == d[:4], i
 
 
 def test_overflow_is_an_error(lib):

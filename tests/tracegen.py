@@ -31,3 +31,23 @@ def random_trace(seed, m, nkeys, configs, fastforward=False, big_n=False, one_cf
     if fastforward:
         sms = (ts // 1_000_000) + np.cumsum(rng.choice([0, 0, 0, 1500], m)).astype(np.int64)
     return keys, ts, n, cfg, sms
+
+
+def skewed_trace(seed, m, nkeys, configs, skews_ns=(0, -2_500_000_000, -7 * NS, 4 * NS, -130 * NS),
+                 big_n=False):
+    """N app servers with skewed clocks sharing one limiter (docs/ARCHITECTURE.md
+    :142-164): requests arrive in true-time order, each stamped with its
+    server's clock (t = true time + skew), so per-key times go back by one or
+    more windows; the Redis clock (server_ms) is the store's own, monotone."""
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, nkeys, m).astype(np.uint64)
+    gaps = rng.choice([0, 1000, 250_000, 50_000_000, 700_000_000], m, p=[0.1, 0.4, 0.2, 0.25, 0.05])
+    true_t = T0 + np.cumsum(gaps).astype(np.int64)
+    server = rng.integers(0, len(skews_ns), m)
+    ts = true_t + np.asarray(skews_ns, np.int64)[server]
+    n = rng.choice([1, 1, 1, 2, 3, 7], m).astype(np.int64)
+    if big_n:
+        n[rng.random(m) < 0.01] = (1 << 62)
+    cfg = (keys % len(configs)).astype(np.uint32)
+    sms = true_t // 1_000_000
+    return keys, ts, n, cfg, sms
