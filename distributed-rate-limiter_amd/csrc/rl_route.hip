@@ -1,0 +1,444 @@
+// rl_route.hip -- the routing kernels of include/rl_route.h: hash-sharded
+// request batches across the GPUs of a node.
+//
+// All byte/integer work, HBM-bound, no MFMA:
+//   pack     owner hash, per-tile owner counts, a one-block scan, a stable
+//            scatter into per-owner groups of 32-byte records (ranks from wave
+//            ballots, as rl_sort.h), so each group is one contiguous all-to-all
+//            chunk
+//   merge    the received records in time order (ties: source rank, source
+//            position) by a stable LSD radix sort of (ts - min ts) as 32-bit
+//            keys -- four one-sweep passes of rl_sort.h's k_sort_pass, digit
+//            histograms fused into the key kernel -- then one gather into the
+//            engine's input arrays
+//   results  / unpack: 32-byte result records gathered by position, written
+//            coalesced
+// Reference: the N app servers sharing one Redis of docs/ARCHITECTURE.md
+// :142-164; the order one shared store applies a key's requests in.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "../../include/rl_route.h"
+#include "rl_sort.h"
+#include "rl_table.h"
+
+using namespace rl;
+
+namespace {
+
+constexpr int RT_BLOCK = 256;
+constexpr int RT_ITEMS = 16;
+constexpr int RT_TILE = RT_BLOCK * RT_ITEMS;   // requests per pack tile
+constexpr int MAX_WORLD = 64;
+constexpr int MERGE_PASSES = 4;                // 32-bit time keys, 8-bit digits
+
+// router status bits (sticky, cleared by rl_router_sync)
+constexpr uint32_t RS_SPAN = 1u;               // received ts span >= 2^32 ns
+
+__device__ inline uint32_t owner_of(uint64_t k, uint32_t world) { return (uint32_t)(mix64(k) >> 32) % world; }
+
+__global__ __launch_bounds__(RT_BLOCK) void k_route_owner(uint32_t m, const uint64_t* __restrict__ key,
+                                                          uint32_t world, uint32_t* __restrict__ owner) {
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK)
+        owner[i] = owner_of(key[i], world);
+}
+
+__device__ inline unsigned long long bias(int64_t t) { return (unsigned long long)t ^ 0x8000000000000000ull; }
+__device__ inline int64_t unbias(unsigned long long u) { return (int64_t)(u ^ 0x8000000000000000ull); }
+
+// per-tile owner counts: tile_cnt[tile * world + o]; the batch's latest ts
+// (biased, atomicMax into *maxts)
+__global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint64_t* __restrict__ key,
+                                                         const int64_t* __restrict__ ts, uint32_t world,
+                                                         uint32_t* __restrict__ tile_cnt,
+                                                         unsigned long long* maxts) {
+    __shared__ uint32_t s_cnt[MAX_WORLD];
+    if (threadIdx.x < MAX_WORLD) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * RT_TILE;
+    unsigned long long hi = 0;
+#pragma unroll
+    for (int j = 0; j < RT_ITEMS; j++) {
+        const uint32_t i = base + j * RT_BLOCK + threadIdx.x;
+        if (i < m) {
+            atomicAdd(&s_cnt[owner_of(key[i], world)], 1u);
+            const unsigned long long b = bias(ts[i]);
+            hi = b > hi ? b : hi;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long h2 = __shfl_xor(hi, off);
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0 && hi) atomicMax(maxts, hi);
+    __syncthreads();
+    if (threadIdx.x < world) tile_cnt[(size_t)blockIdx.x * world + threadIdx.x] = s_cnt[threadIdx.x];
+}
+
+// one block: tile_cnt -> per-(tile, owner) output offsets (in place), the
+// {count, latest ts} pair per owner (int64, for the count all-to-all)
+__global__ void k_route_scan(uint32_t tiles, uint32_t world, uint32_t* __restrict__ tile_cnt,
+                             const unsigned long long* maxts, int64_t* __restrict__ info) {
+    __shared__ uint32_t s_tot[MAX_WORLD];
+    const uint32_t o = threadIdx.x;
+    uint32_t run = 0;
+    if (o < world) {
+        for (uint32_t t = 0; t < tiles; t++) {
+            const uint32_t c = tile_cnt[(size_t)t * world + o];
+            tile_cnt[(size_t)t * world + o] = run;
+            run += c;
+        }
+        s_tot[o] = run;
+        info[2 * o] = run;
+        info[2 * o + 1] = unbias(*maxts);
+    }
+    __syncthreads();
+    if (o < world) {
+        uint32_t base = 0;
+        for (uint32_t q = 0; q < o; q++) base += s_tot[q];
+        for (uint32_t t = 0; t < tiles; t++) tile_cnt[(size_t)t * world + o] += base;
+    }
+}
+
+// stable scatter of the requests into per-owner groups
+__global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(uint32_t m, const uint64_t* __restrict__ key,
+                                                            const int64_t* __restrict__ ts,
+                                                            const int64_t* __restrict__ n,
+                                                            const uint32_t* __restrict__ cfg, uint32_t world,
+                                                            const uint32_t* __restrict__ tile_off,
+                                                            rl_route_rec* __restrict__ send,
+                                                            uint32_t* __restrict__ slot) {
+    constexpr int W = RT_BLOCK / 64;
+    __shared__ uint32_t s_wcnt[W][MAX_WORLD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (int k = tid; k < W * MAX_WORLD; k += RT_BLOCK) (&s_wcnt[0][0])[k] = 0;
+    __syncthreads();
+    // wave w takes the tile's requests [w * 64 * RT_ITEMS, (w + 1) * 64 * RT_ITEMS) in order
+    const uint32_t base = blockIdx.x * RT_TILE + wave * (64 * RT_ITEMS);
+    uint32_t own[RT_ITEMS], rank[RT_ITEMS];
+    const uint64_t lt = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int j = 0; j < RT_ITEMS; j++) {
+        const uint32_t i = base + j * 64 + lane;
+        const bool ok = i < m;
+        own[j] = ok ? owner_of(key[i], world) : 0u;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 6; b++) {   // world <= 64: match the 6-bit owner id
+            const uint32_t bit = (own[j] >> b) & 1u;
+            const uint64_t bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        if (ok) {
+            const uint32_t below = __popcll(peers & lt);
+            const uint32_t cur = s_wcnt[wave][own[j]];
+            rank[j] = cur + below;
+            if (below == 0) s_wcnt[wave][own[j]] = cur + (uint32_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+    // per owner: exclusive prefix over the waves, plus the tile's offset
+    if (tid < (int)world) {
+        uint32_t run = tile_off[(size_t)blockIdx.x * world + tid];
+        for (int w = 0; w < W; w++) {
+            const uint32_t c = s_wcnt[w][tid];
+            s_wcnt[w][tid] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < RT_ITEMS; j++) {
+        const uint32_t i = base + j * 64 + lane;
+        if (i >= m) continue;
+        const uint32_t p = s_wcnt[wave][own[j]] + rank[j];
+        rl_route_rec r;
+        r.key = key[i];
+        r.ts = ts[i];
+        r.n = n[i];
+        r.cfg = cfg[i];
+        r.pos = i;
+        send[p] = r;
+        slot[i] = p;
+    }
+}
+
+// ctrl layout of the merge: [0,1] min ts (biased u64), [2,3] max ts, [4] status,
+// [8 .. 8 + 4*256) digit histograms, then 4 tile counters
+constexpr uint32_t MC_MIN = 0, MC_MAX = 2, MC_STATUS = 4, MC_HIST = 8;
+constexpr uint32_t MC_TILE = MC_HIST + MERGE_PASSES * RADIX;
+constexpr uint32_t MC_WORDS = MC_TILE + MERGE_PASSES;
+
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_minmax(uint32_t m, const rl_route_rec* __restrict__ rec,
+                                                           uint32_t* ctrl) {
+    unsigned long long lo = ~0ull, hi = 0ull;
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
+        const unsigned long long b = bias(rec[i].ts);
+        lo = b < lo ? b : lo;
+        hi = b > hi ? b : hi;
+    }
+    // wave reduction, then one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin((unsigned long long*)(ctrl + MC_MIN), lo);
+        atomicMax((unsigned long long*)(ctrl + MC_MAX), hi);
+    }
+}
+
+// 32-bit time key (ts - min) of every received record + the digit histograms
+// of the four passes
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_route_rec* __restrict__ rec,
+                                                         uint32_t* ctrl, uint32_t* __restrict__ kout) {
+    __shared__ uint32_t lh[MERGE_PASSES][RADIX];
+    for (int p = 0; p < MERGE_PASSES; p++) lh[p][threadIdx.x] = 0;
+    __syncthreads();
+    const int64_t tmin = unbias(*(const unsigned long long*)(ctrl + MC_MIN));
+    const int64_t tmax = unbias(*(const unsigned long long*)(ctrl + MC_MAX));
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (uint64_t)(tmax - tmin) > 0xffffffffull)
+        atomicOr(ctrl + MC_STATUS, RS_SPAN);
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
+        const uint32_t k = (uint32_t)(uint64_t)(rec[i].ts - tmin);
+        kout[i] = k;
+#pragma unroll
+        for (int p = 0; p < MERGE_PASSES; p++) atomicAdd(&lh[p][(k >> (8 * p)) & (RADIX - 1)], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < MERGE_PASSES; p++) {
+        const uint32_t v = lh[p][threadIdx.x];
+        if (v) atomicAdd(&ctrl[MC_HIST + p * RADIX + threadIdx.x], v);
+    }
+}
+
+// sorted position p holds received record v[p]: the engine's inputs in
+// order, with the store clock max(floor(ts / 1e6), clock of earlier steps)
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uint32_t* __restrict__ v,
+                                                           const rl_route_rec* __restrict__ rec,
+                                                           const int64_t* __restrict__ clock,
+                                                           uint64_t* __restrict__ key, int64_t* __restrict__ ts,
+                                                           int64_t* __restrict__ n, uint32_t* __restrict__ cfg,
+                                                           int64_t* __restrict__ sms, uint32_t* __restrict__ at) {
+    const int64_t c0 = *clock;
+    for (uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x; p < m; p += gridDim.x * RT_BLOCK) {
+        const uint32_t i = v[p];
+        const rl_route_rec r = rec[i];
+        key[p] = r.key;
+        ts[p] = r.ts;
+        n[p] = r.n;
+        cfg[p] = r.cfg;
+        const int64_t ms = floor_div(r.ts, 1000000LL);
+        sms[p] = ms > c0 ? ms : c0;
+        at[i] = p;
+    }
+}
+
+// after a step: clock = max(clock, floor(latest ts of any rank / 1e6))
+__global__ void k_merge_clock(uint32_t world, const int64_t* __restrict__ info, int64_t* clock) {
+    int64_t c = *clock;
+    for (uint32_t r = 0; r < world; r++) {
+        if (info[2 * r + 1] == INT64_MIN) continue;   // that rank's batch was empty
+        const int64_t ms = floor_div(info[2 * r + 1], 1000000LL);
+        c = ms > c ? ms : c;
+    }
+    *clock = c;
+}
+
+__global__ __launch_bounds__(RT_BLOCK) void k_route_results(uint32_t m, const uint32_t* __restrict__ at,
+                                                            const uint8_t* __restrict__ dec,
+                                                            const int64_t* __restrict__ rem,
+                                                            const int64_t* __restrict__ retry,
+                                                            const int64_t* __restrict__ reset,
+                                                            rl_route_res* __restrict__ res) {
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
+        const uint32_t p = at[i];
+        res[i] = rl_route_res{(int64_t)dec[p], rem[p], retry[p], reset[p]};
+    }
+}
+
+__global__ __launch_bounds__(RT_BLOCK) void k_route_unpack(uint32_t m, const uint32_t* __restrict__ slot,
+                                                           const rl_route_res* __restrict__ back,
+                                                           uint8_t* __restrict__ dec, int64_t* __restrict__ rem,
+                                                           int64_t* __restrict__ retry,
+                                                           int64_t* __restrict__ reset) {
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
+        const rl_route_res r = back[slot[i]];
+        dec[i] = (uint8_t)r.decision;
+        rem[i] = r.remaining;
+        retry[i] = r.retry_after_ns;
+        reset[i] = r.reset_at_ns;
+    }
+}
+
+int grid_for(size_t m) { return (int)std::min<size_t>((m + RT_BLOCK - 1) / RT_BLOCK, 2048); }
+
+}  // namespace
+
+struct rl_router {
+    int device = 0;
+    uint32_t world = 1, max_batch = 0, max_recv = 0;
+    uint32_t* tile_cnt = nullptr;    // pack: [tiles][world]
+    uint32_t* ctrl = nullptr;        // merge: MC_* words + look-back status
+    uint32_t* status = nullptr;      // merge: [MERGE_PASSES][tiles][RADIX]
+    size_t ctrl_bytes = 0;
+    uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr;
+    uint32_t* d_status = nullptr;    // sticky router status (RS_*)
+    int64_t* clock = nullptr;         // the store clock of the next step (ms)
+    unsigned long long* maxts = nullptr;   // pack: the batch's latest ts (biased)
+};
+
+extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t max_recv,
+                                rl_router** out) {
+    if (!out || world < 1 || world > MAX_WORLD || max_batch == 0 || max_recv == 0 || max_batch > (1u << 30) ||
+        max_recv > (1u << 30))
+        return RL_EINVAL;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return RL_EDEVICE;
+    rl_router* r = new rl_router();
+    r->device = device;
+    r->world = (uint32_t)world;
+    r->max_batch = max_batch;
+    r->max_recv = max_recv;
+    const size_t ptiles = (max_batch + RT_TILE - 1) / RT_TILE;
+    const size_t stiles = (max_recv + SORT_TILE - 1) / SORT_TILE;
+    r->ctrl_bytes = 4 * (MC_WORDS + (size_t)MERGE_PASSES * stiles * RADIX);
+    bool ok = hipMalloc(&r->tile_cnt, 4 * ptiles * world) == hipSuccess;
+    ok = ok && hipMalloc(&r->ctrl, r->ctrl_bytes) == hipSuccess;
+    for (uint32_t** p : {&r->k0, &r->k1, &r->v0, &r->v1}) ok = ok && hipMalloc(p, 4 * (size_t)max_recv) == hipSuccess;
+    ok = ok && hipMalloc(&r->d_status, 4) == hipSuccess && hipMemset(r->d_status, 0, 4) == hipSuccess;
+    ok = ok && hipMalloc(&r->maxts, 8) == hipSuccess;
+    if (ok && hipMalloc(&r->clock, 8) == hipSuccess) {
+        const int64_t lo = INT64_MIN;
+        ok = hipMemcpy(r->clock, &lo, 8, hipMemcpyHostToDevice) == hipSuccess;
+    } else {
+        ok = false;
+    }
+    if (!ok) {
+        rl_router_destroy(r);
+        return RL_ENOMEM;
+    }
+    r->status = r->ctrl + MC_WORDS;
+    *out = r;
+    return RL_OK;
+}
+
+extern "C" int rl_router_destroy(rl_router* r) {
+    if (!r) return RL_EINVAL;
+    (void)hipSetDevice(r->device);
+    for (void* p : {(void*)r->tile_cnt, (void*)r->ctrl, (void*)r->k0, (void*)r->k1, (void*)r->v0, (void*)r->v1,
+                    (void*)r->d_status, (void*)r->clock, (void*)r->maxts})
+        (void)hipFree(p);
+    delete r;
+    return RL_OK;
+}
+
+extern "C" int rl_router_sync(rl_router* r, void* stream) {
+    if (!r) return RL_EINVAL;
+    (void)hipSetDevice(r->device);
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return RL_EDEVICE;
+    uint32_t s = 0;
+    if (hipMemcpy(&s, r->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess) return RL_EDEVICE;
+    if (hipMemset(r->d_status, 0, 4) != hipSuccess) return RL_EDEVICE;
+    if (s & EF_LOOKBACK) return RL_ETIMEOUT;
+    if (s & (RS_SPAN << 8)) return RL_EINVAL;
+    return RL_OK;
+}
+
+extern "C" int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner, void* stream) {
+    if (!r || (m && (!key || !owner)) || m > r->max_batch) return RL_EINVAL;
+    if (!m) return RL_OK;
+    (void)hipSetDevice(r->device);
+    k_route_owner<<<grid_for(m), RT_BLOCK, 0, (hipStream_t)stream>>>((uint32_t)m, key, r->world, owner);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+extern "C" int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
+                             const uint32_t* cfg, rl_route_rec* send, int64_t* send_info, uint32_t* slot,
+                             void* stream) {
+    if (!r || !send_info || m > r->max_batch || (m && (!key || !ts || !n || !cfg || !send || !slot)))
+        return RL_EINVAL;
+    (void)hipSetDevice(r->device);
+    hipStream_t s = (hipStream_t)stream;
+    // latest ts starts at biased INT64_MIN (0): an empty batch reports INT64_MIN
+    if (hipMemsetAsync(r->maxts, 0, 8, s) != hipSuccess) return RL_EDEVICE;
+    const uint32_t tiles = (uint32_t)((m + RT_TILE - 1) / RT_TILE);
+    if (m) k_route_hist<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, r->world, r->tile_cnt, r->maxts);
+    k_route_scan<<<1, MAX_WORLD, 0, s>>>(tiles, r->world, r->tile_cnt, r->maxts, send_info);
+    if (!m) return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+    k_route_scatter<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, n, cfg, r->world, r->tile_cnt, send, slot);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+__global__ void k_merge_init(uint32_t* ctrl) {
+    *(unsigned long long*)(ctrl + MC_MIN) = ~0ull;
+    *(unsigned long long*)(ctrl + MC_MAX) = 0ull;
+}
+
+__global__ void k_merge_status(const uint32_t* ctrl, const uint32_t* sort_flags, uint32_t* status) {
+    const uint32_t s = (ctrl[MC_STATUS] << 8) | (*sort_flags & EF_LOOKBACK);
+    if (s) atomicOr(status, s);
+}
+
+extern "C" int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info,
+                              uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg, int64_t* server_ms, uint32_t* at,
+                              void* stream) {
+    if (!r || !recv_info || m_recv > r->max_recv ||
+        (m_recv && (!recv || !key || !ts || !n || !cfg || !server_ms || !at)))
+        return RL_EINVAL;
+    (void)hipSetDevice(r->device);
+    hipStream_t s = (hipStream_t)stream;
+    if (!m_recv) {
+        k_merge_clock<<<1, 1, 0, s>>>(r->world, recv_info, r->clock);
+        return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+    }
+    const uint32_t m = (uint32_t)m_recv;
+    const uint32_t stiles = (m + SORT_TILE - 1) / SORT_TILE;
+    if (hipMemsetAsync(r->ctrl, 0, r->ctrl_bytes, s) != hipSuccess) return RL_EDEVICE;
+    k_merge_init<<<1, 1, 0, s>>>(r->ctrl);
+    k_merge_minmax<<<grid_for(m), RT_BLOCK, 0, s>>>(m, recv, r->ctrl);
+    k_merge_keys<<<grid_for(m), RT_BLOCK, 0, s>>>(m, recv, r->ctrl, r->k0);
+    // look-back timeouts of the sort land in ctrl[MC_STATUS + 1] (EF_LOOKBACK)
+    uint32_t* sflags = r->ctrl + MC_STATUS + 1;
+    uint32_t *kin = r->k0, *vin = r->v0, *kout = r->k1, *vout = r->v1;
+    const size_t max_stiles = (r->max_recv + SORT_TILE - 1) / SORT_TILE;
+    for (int p = 0; p < MERGE_PASSES; p++) {
+        uint32_t* st = r->status + (size_t)p * max_stiles * RADIX;
+        if (p == 0)
+            k_sort_pass<true><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, r->ctrl + MC_HIST + p * RADIX,
+                                                            st, r->ctrl + MC_TILE + p, sflags);
+        else
+            k_sort_pass<false><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p,
+                                                             r->ctrl + MC_HIST + p * RADIX, st,
+                                                             r->ctrl + MC_TILE + p, sflags);
+        std::swap(kin, kout);
+        std::swap(vin, vout);
+    }
+    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, vin, recv, r->clock, key, ts, n, cfg, server_ms, at);
+    k_merge_clock<<<1, 1, 0, s>>>(r->world, recv_info, r->clock);
+    k_merge_status<<<1, 1, 0, s>>>(r->ctrl, sflags, r->d_status);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+extern "C" int rl_route_results(size_t m_recv, const uint32_t* at, const uint8_t* decision, const int64_t* remaining,
+                                const int64_t* retry_after_ns, const int64_t* reset_at_ns, rl_route_res* res,
+                                void* stream) {
+    if (m_recv > (1u << 30) || (m_recv && (!at || !decision || !remaining || !retry_after_ns || !reset_at_ns || !res)))
+        return RL_EINVAL;
+    if (!m_recv) return RL_OK;
+    k_route_results<<<grid_for(m_recv), RT_BLOCK, 0, (hipStream_t)stream>>>((uint32_t)m_recv, at, decision, remaining,
+                                                                            retry_after_ns, reset_at_ns, res);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+extern "C" int rl_route_unpack(size_t m, const uint32_t* slot, const rl_route_res* back, uint8_t* decision,
+                               int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns, void* stream) {
+    if (m > (1u << 30) || (m && (!slot || !back || !decision || !remaining || !retry_after_ns || !reset_at_ns)))
+        return RL_EINVAL;
+    if (!m) return RL_OK;
+    k_route_unpack<<<grid_for(m), RT_BLOCK, 0, (hipStream_t)stream>>>((uint32_t)m, slot, back, decision, remaining,
+                                                                      retry_after_ns, reset_at_ns);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}

@@ -151,45 +151,6 @@ __global__ void k_rehash(const E* __restrict__ old, uint64_t n_old, E* nu, uint6
 
 __device__ inline uint64_t spill_home(uint64_t k, uint64_t mask) { return mix64(k ^ 0x5bd1e9955bd1e995ULL) & mask; }
 
-// Table GC of the spill table, after the window table's k_rehash: every live
-// spill entry moves to the fresh spill table (strict CAS: two entries of one
-// user key may be moved at once) and is counted in its user key's new window
-// entry.  counters as k_rehash.
-__global__ void k_spill_rehash(const SpillEntry* __restrict__ old, uint64_t n_old, SpillEntry* nu, uint64_t mask_new,
-                               WinEntry* win, uint64_t win_mask, int64_t now_ms, int32_t profile,
-                               unsigned long long* counters) {
-    unsigned long long live = 0, lost = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n_old;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const SpillEntry x = old[i];
-        if (!entry_live(x, now_ms, profile)) continue;
-        live++;
-        const uint32_t w = probe_find(win, win_mask, x.key);
-        uint64_t h = spill_home(x.key, mask_new);
-        bool placed = false;
-        for (uint64_t p = 0; w != NO_SLOT && p <= mask_new && p < MAX_PROBES; p++) {
-            if (atomicCAS((unsigned long long*)&nu[h].key, (unsigned long long)EMPTY_KEY,
-                          (unsigned long long)x.key) == EMPTY_KEY) {
-                nu[h].ws = x.ws;
-                nu[h].cnt = x.cnt;
-                nu[h].when = x.when;
-                atomicAdd((unsigned long long*)&win[w].nspill, 1ull);
-                placed = true;
-                break;
-            }
-            h = (h + 1) & mask_new;
-        }
-        if (!placed) lost++;
-    }
-    if (live) atomicAdd(&counters[0], live);
-    if (lost) atomicAdd(&counters[1], lost);
-}
-
-__global__ void k_init_spill(SpillEntry* t, uint64_t n) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        t[i] = SpillEntry{EMPTY_KEY, 0, 0, ABSENT};
-}
-
 // occupied and live entries (rl_table_info_get)
 template <typename E>
 __global__ void k_table_count(const E* __restrict__ t, uint64_t n, int64_t now_ms, int32_t profile,

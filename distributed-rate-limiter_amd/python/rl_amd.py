@@ -146,6 +146,14 @@ _sig = {
     "rl_decide_batch_keys_device": (C.c_int, [vp, C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p,
                                               C.c_size_t] + [vp] * 10),
     "rl_hash_keys": (C.c_int, [C.c_int32, C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_size_t, vp]),
+    "rl_router_create": (C.c_int, [C.c_int32, C.c_int32, C.c_uint32, C.c_uint32, C.POINTER(vp)]),
+    "rl_router_destroy": (C.c_int, [vp]),
+    "rl_router_sync": (C.c_int, [vp, vp]),
+    "rl_route_owner": (C.c_int, [vp, C.c_size_t, vp, vp, vp]),
+    "rl_route_pack": (C.c_int, [vp, C.c_size_t] + [vp] * 8),
+    "rl_route_merge": (C.c_int, [vp, C.c_size_t] + [vp] * 9),
+    "rl_route_results": (C.c_int, [C.c_size_t] + [vp] * 7),
+    "rl_route_unpack": (C.c_int, [C.c_size_t] + [vp] * 7),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -291,6 +299,59 @@ class Engine:
         if rc != RL_OK:
             raise EngineError(rc, self.last_error())
         return out
+
+
+class Router:
+    """rl_router (include/rl_route.h): the routing kernels of one rank.  All
+    arguments are device pointers (ints) and a hipStream_t; asynchronous."""
+
+    def __init__(self, device, world, max_batch, max_recv):
+        h = vp()
+        rc = lib.rl_router_create(device, world, max_batch, max_recv, C.byref(h))
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_router_create failed")
+        self.h = h
+        self.world = world
+
+    def _chk(self, rc, what):
+        if rc != RL_OK:
+            raise EngineError(rc, what)
+
+    def owner(self, m, key, owner, stream):
+        self._chk(lib.rl_route_owner(self.h, m, key, owner, stream), "rl_route_owner")
+
+    def pack(self, m, key, ts, n, cfg, send, send_info, slot, stream):
+        self._chk(lib.rl_route_pack(self.h, m, key, ts, n, cfg, send, send_info, slot, stream), "rl_route_pack")
+
+    def merge(self, m_recv, recv, recv_info, key, ts, n, cfg, sms, at, stream):
+        self._chk(lib.rl_route_merge(self.h, m_recv, recv, recv_info, key, ts, n, cfg, sms, at, stream),
+                  "rl_route_merge")
+
+    @staticmethod
+    def results(m_recv, at, dec, rem, retry, reset, res, stream):
+        rc = lib.rl_route_results(m_recv, at, dec, rem, retry, reset, res, stream)
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_route_results")
+
+    @staticmethod
+    def unpack(m, slot, back, dec, rem, retry, reset, stream):
+        rc = lib.rl_route_unpack(m, slot, back, dec, rem, retry, reset, stream)
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_route_unpack")
+
+    def sync(self, stream=None) -> int:
+        return lib.rl_router_sync(self.h, stream)
+
+    def close(self):
+        if self.h:
+            lib.rl_router_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # --- host mirror of the Go API (include/rl_limiter.h) ------------------------

@@ -1,22 +1,21 @@
 """Key-space sharding across GPUs (one process per GPU, torch.distributed).
 
 Each rank owns the keys with owner(key) == rank (a 64-bit mix of the key id,
-mod world size) and keeps their state in its own HBM tables.  Two ways to
-feed it:
+mod world size, include/rl_route.h) and keeps their state in its own HBM
+tables.  Two ways to feed it:
 
-  * sharded ingress (bench.py --gpus N): every rank receives only requests of
-    the keys it owns; no data-path collective, weak scaling;
-  * routed ingress (route_and_decide_torch, device-resident; route_and_decide,
-    its host-side numpy twin): every rank receives arbitrary requests; one
-    all-to-all moves each request record (key, ts, n, cfg, and its position)
-    to its owner, the owner decides, and the inverse all-to-all returns the
-    results.  On MI355X the "nccl" backend is RCCL over xGMI, where
-    all-to-all drives all 7 point-to-point links at once.
+  * routed ingress (RoutedPipeline, bench.py --gpus N): every rank receives
+    arbitrary requests; the routing kernels group them by owner, an all-to-all
+    moves the request records to their owners, the owner decides, and the
+    inverse all-to-all returns the results.  On MI355X the "nccl" backend is
+    RCCL over xGMI, where all-to-all drives all 7 point-to-point links at once;
+  * sharded ingress (bench.py --ingress sharded): every rank receives only
+    requests of the keys it owns; no data-path collective (N replicas).
 
-Order: the reference's N app servers share one Redis, which sees requests in
-arrival order.  The owner replays the union of the ranks' requests ordered by
-(ts, source rank, source position), a deterministic total order consistent
-with each rank's own order.
+Order: the reference's N app servers share one Redis, which applies a key's
+requests in arrival order.  The owner replays the union of the ranks'
+requests ordered by (ts, source rank, source position), a deterministic total
+order consistent with each rank's own order, under one monotone store clock.
 """
 from __future__ import annotations
 
@@ -45,100 +44,163 @@ def owner_of(key: np.ndarray, world: int) -> np.ndarray:
     return ((mix64(key) >> np.uint64(32)) % np.uint64(world)).astype(np.int64)
 
 
-def _a2a(send: torch.Tensor, send_counts, recv_counts, group=None) -> torch.Tensor:
-    out = torch.empty((int(sum(recv_counts)),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
-    dist.all_to_all_single(out, send, output_split_sizes=list(recv_counts),
-                           input_split_sizes=list(send_counts), group=group)
-    return out
+# --- the native routed pipeline (include/rl_route.h) ---------------------------
+
+def _ctx(stream):
+    import contextlib
+    return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
 
 
-def route_and_decide(key, ts, n, cfg, decide, device="cpu", group=None):
-    """Route this rank's requests to their owners, decide there, return the
-    results in this rank's original order.
+class RoutedPipeline:
+    """One rank of the routed decision path: every rank accepts requests for
+    any key; the routing kernels (include/rl_route.h: `ops`, an rl_amd.Router)
+    group them by owner GPU, two RCCL all-to-alls over xGMI (torch.distributed
+    "nccl" process groups) move request records to their owners and results
+    back, and the owner's engine decides its keys in the order one shared
+    store sees them -- by request time, ties by (source rank, source position).
 
-    decide(key, ts, n, cfg) -> (decision u8, remaining i64, retry i64, reset i64)
-    runs on the owner over the merged, ordered requests it received.
-    """
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    m = key.size
-    own = owner_of(key, world)
-    order = np.argsort(own, kind="stable")
-    send_counts = np.bincount(own, minlength=world)
-    # record: key, ts, n, cfg, src position (int64 each)
-    rec = np.stack([key.view(np.int64), ts, n, cfg.astype(np.int64), np.arange(m, dtype=np.int64)], axis=1)[order]
-    cnt_t = torch.tensor(send_counts, dtype=torch.int64, device=device)
-    recv_t = torch.empty_like(cnt_t)
-    dist.all_to_all_single(recv_t, cnt_t, group=group)
-    recv_counts = recv_t.cpu().numpy()
-    got = _a2a(torch.from_numpy(rec).to(device), send_counts, recv_counts, group).cpu().numpy()
-    src = np.repeat(np.arange(world), recv_counts)
-    # owner-side total order: (ts, source rank, source position)
-    o = np.lexsort((got[:, 4], src, got[:, 1]))
-    g = got[o]
-    dec, rem, retry, reset = decide(g[:, 0].view(np.uint64).copy(), g[:, 1].copy(), g[:, 2].copy(),
-                                    g[:, 3].astype(np.uint32))
-    res = np.empty((g.shape[0], 4), np.int64)
-    res[o] = np.stack([dec.astype(np.int64), rem, retry, reset], axis=1)  # back to arrival-from-src order
-    back = _a2a(torch.from_numpy(res).to(device), recv_counts, send_counts, group).cpu().numpy()
-    out = np.empty((m, 4), np.int64)
-    out[order] = back
-    return out[:, 0].astype(np.uint8), out[:, 1], out[:, 2], out[:, 3]
+    Pipelining: batch b's pack and count exchange (stage A) are issued
+    `lookahead` steps before its records move (stage B), so the host reads the
+    counts that size the record all-to-all from a finished copy instead of
+    stalling the GPU.  `depth` buffer sets rotate; a set is rewritten only
+    after the batch that used it `depth` steps earlier has finished.  Requests go through their own process group and stream;
+    results through a second group and one of `depth` streams, so a batch's
+    result exchange never holds up the next batches' request exchange.
 
+    decide(m, key, ts, n, cfg, sms, dec, rem, retry, reset, stream) enqueues
+    the engine on the owner's merged requests (device pointers; the engine's
+    rl_decide_batch_device without RL_OPT_PIPELINE: its grouping waits for
+    `stream`, which has waited for the merge).  sms: the store clock
+    (include/rl_route.h), the same on every owner."""
 
-def _i64(c: int) -> int:
-    """a 64-bit constant as the signed value torch's int64 arithmetic uses"""
-    return c - (1 << 64) if c >= (1 << 63) else c
+    def __init__(self, ops, decide, world, max_batch, device, pg_req=None, pg_res=None, depth=6, lookahead=2,
+                 max_recv=None, staged=False):
+        self.ops, self.decide, self.world = ops, decide, world
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.pg_req, self.pg_res = pg_req, pg_res
+        self.depth, self.lookahead = depth, lookahead
+        self.staged = staged          # all-to-alls through host memory (gloo with device tensors)
+        mb = max_batch
+        mr = max_recv or world * max_batch
+        self.max_batch, self.max_recv = mb, mr
+        d = self.dev
+        self.R = torch.cuda.Stream(d) if self.cuda else None
+        self.slots = []
+        for _ in range(depth):
+            s = dict(
+                send=torch.empty((mb, 4), dtype=torch.int64, device=d),
+                slot=torch.empty(mb, dtype=torch.int32, device=d),
+                scnt=torch.zeros((world, 2), dtype=torch.int64, device=d),   # {count, latest ts} per owner
+                rcnt=torch.zeros((world, 2), dtype=torch.int64, device=d),   # {count, latest ts} per source
+                cnt_h=torch.zeros((2, world, 2), dtype=torch.int64, pin_memory=self.cuda),
+                recv=torch.empty((mr, 4), dtype=torch.int64, device=d),
+                key=torch.empty(mr, dtype=torch.int64, device=d),
+                ts=torch.empty(mr, dtype=torch.int64, device=d),
+                n=torch.empty(mr, dtype=torch.int64, device=d),
+                cfg=torch.empty(mr, dtype=torch.int32, device=d),
+                sms=torch.empty(mr, dtype=torch.int64, device=d),
+                at=torch.empty(mr, dtype=torch.int32, device=d),
+                dec=torch.empty(mr, dtype=torch.uint8, device=d),
+                rem=torch.empty(mr, dtype=torch.int64, device=d),
+                retry=torch.empty(mr, dtype=torch.int64, device=d),
+                reset=torch.empty(mr, dtype=torch.int64, device=d),
+                res=torch.empty((mr, 4), dtype=torch.int64, device=d),
+                back=torch.empty((mb, 4), dtype=torch.int64, device=d),
+                S=torch.cuda.Stream(d) if self.cuda else None,
+                ev_cnt=None, ev_merged=None, ev_done=None, m=0, busy=False,
+            )
+            self.slots.append(s)
+        self.last_recv = 0
 
+    @staticmethod
+    def _p(t):
+        return t.data_ptr()
 
-def mix64_torch(x: torch.Tensor) -> torch.Tensor:
-    """splitmix64 finalizer on int64 tensors (wrapping multiply, logical shifts)."""
-    def shr(v, k):
-        return (v >> k) & ((1 << (64 - k)) - 1)
-    x = x ^ shr(x, 30)
-    x = x * _i64(0xbf58476d1ce4e5b9)
-    x = x ^ shr(x, 27)
-    x = x * _i64(0x94d049bb133111eb)
-    x = x ^ shr(x, 31)
-    return x
+    def _sp(self, stream):
+        return stream.cuda_stream if stream is not None else None
 
+    def _a2a(self, out, inp, out_splits, in_splits, group):
+        if self.staged:
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                                   group=group)
+            out.copy_(o, non_blocking=False)
+        else:
+            dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
 
-def owner_of_torch(key: torch.Tensor, world: int) -> torch.Tensor:
-    """owner_of for int64 tensors holding the u64 key ids (same partition)."""
-    hi = (mix64_torch(key) >> 32) & 0xffffffff
-    return hi % world
+    def stage_a(self, b, key, ts, n, cfg):
+        """pack batch b (device tensors: key/ts/n int64, cfg int32; complete
+        now) and exchange its owner counts"""
+        s = self.slots[b % self.depth]
+        assert not s["busy"], "pipeline slot reused before its stage B"
+        m = key.numel()
+        assert m <= self.max_batch
+        s["m"], s["busy"] = m, True
+        p = self._p
+        with _ctx(self.R):
+            if s["ev_done"] is not None:
+                self.R.wait_event(s["ev_done"])   # the set's previous batch has finished
+            self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]),
+                          self._sp(self.R))
+            self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_req)
+            s["cnt_h"][0].copy_(s["scnt"], non_blocking=True)
+            s["cnt_h"][1].copy_(s["rcnt"], non_blocking=True)
+            if self.cuda:
+                s["ev_cnt"] = torch.cuda.Event()
+                s["ev_cnt"].record(self.R)
 
+    def stage_b(self, b, dec, rem, retry, reset):
+        """move batch b's requests, decide them at their owners, bring the
+        results back into dec/rem/retry/reset (device tensors, batch order);
+        returns the stream on which they are complete"""
+        s = self.slots[b % self.depth]
+        if s["ev_cnt"] is not None:
+            s["ev_cnt"].synchronize()
+        sc = s["cnt_h"][0][:, 0].tolist()
+        rc = s["cnt_h"][1][:, 0].tolist()
+        tot, m = int(sum(rc)), s["m"]
+        assert tot <= self.max_recv, "received more than max_recv"
+        self.last_recv = tot
+        p = self._p
+        with _ctx(self.R):
+            self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
+            self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]),
+                           p(s["sms"]), p(s["at"]), self._sp(self.R))
+            if self.cuda:
+                s["ev_merged"] = torch.cuda.Event()
+                s["ev_merged"].record(self.R)
+        S = s["S"]
+        with _ctx(S):
+            if S is not None:
+                S.wait_event(s["ev_merged"])
+            self.decide(tot, p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]), p(s["sms"]), p(s["dec"]),
+                        p(s["rem"]), p(s["retry"]), p(s["reset"]), self._sp(S))
+            self.ops.results(tot, p(s["at"]), p(s["dec"]), p(s["rem"]), p(s["retry"]), p(s["reset"]), p(s["res"]),
+                             self._sp(S))
+            self._a2a(s["back"][:m], s["res"][:tot], sc, rc, self.pg_res)
+            self.ops.unpack(m, p(s["slot"]), p(s["back"]), p(dec), p(rem), p(retry), p(reset), self._sp(S))
+            if S is not None:
+                s["ev_done"] = torch.cuda.Event()
+                s["ev_done"].record(S)
+        s["busy"] = False
+        return S
 
-def route_and_decide_torch(key, ts, n, cfg, decide, group=None):
-    """route_and_decide with every step on the tensors' device: owner hash,
-    grouping by owner, the request all-to-all, the owner's (ts, source rank,
-    source position) order, the decision, the inverse all-to-all.
+    def run(self, batches, outs, done=None):
+        """all batches through the pipeline: batches[b] = (key, ts, n, cfg),
+        outs[b] = (dec, rem, retry, reset); `done(b, stream)` after each"""
+        nb = len(batches)
+        L = min(self.lookahead, self.depth - 1)
+        self.prime(batches, L)
+        for b in range(nb):
+            if b + L < nb:
+                self.stage_a(b + L, *batches[b + L])
+            S = self.stage_b(b, *outs[b])
+            if done is not None:
+                done(b, S)
 
-    key, ts, n: int64 tensors (key holds the u64 ids); cfg: int32.
-    decide(key, ts, n, cfg) -> (decision u8, remaining, retry, reset) tensors
-    on the same device, over the merged, ordered requests this rank owns.
-    Returns the four result tensors in this rank's original order.
-    """
-    world = dist.get_world_size(group)
-    dev = key.device
-    m = key.numel()
-    own = owner_of_torch(key, world)
-    order = torch.argsort(own, stable=True)
-    send_counts = torch.bincount(own, minlength=world)
-    rec = torch.stack([key, ts, n, cfg.to(torch.int64), torch.arange(m, dtype=torch.int64, device=dev)], 1)[order]
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    sc, rc = send_counts.tolist(), recv_counts.tolist()
-    got = _a2a(rec, sc, rc, group)
-    # received records are grouped by source rank, each in source order: a
-    # stable sort by ts gives the (ts, source rank, source position) order
-    o = torch.sort(got[:, 1], stable=True).indices
-    g = got[o]
-    dec, rem, retry, reset = decide(g[:, 0].contiguous(), g[:, 1].contiguous(), g[:, 2].contiguous(),
-                                    g[:, 3].to(torch.int32).contiguous())
-    res = torch.empty((g.shape[0], 4), dtype=torch.int64, device=dev)
-    res[o] = torch.stack([dec.to(torch.int64), rem, retry, reset], 1)
-    back = _a2a(res, rc, sc, group)
-    out = torch.empty((m, 4), dtype=torch.int64, device=dev)
-    out[order] = back
-    return out[:, 0].to(torch.uint8), out[:, 1], out[:, 2], out[:, 3]
+    def prime(self, batches, L=None):
+        L = min(self.lookahead, self.depth - 1) if L is None else L
+        nb = len(batches)
+        for b in range(min(L, nb)):
+            self.stage_a(b, *batches[b])

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("rl_engine.h", "rl_limiter.h", "rl_coalescer.h", "rl_keyhash.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h")]
 
 
 def declared_functions():
@@ -24,7 +24,8 @@ def test_headers_declare_the_boundary():
     names = declared_functions()
     for must in ["rl_engine_create", "rl_engine_destroy", "rl_config_register", "rl_decide_batch",
                  "rl_decide_batch_device", "rl_reset", "rl_last_error", "rll_new", "rll_allow_n",
-                 "rl_coalescer_create", "rl_coalescer_submit", "rl_coalescer_wait"]:
+                 "rl_coalescer_create", "rl_coalescer_submit", "rl_coalescer_wait", "rl_route_pack",
+                 "rl_route_merge", "rl_route_results", "rl_route_unpack"]:
         assert must in names
 
 

@@ -2,8 +2,9 @@
 requests to the key's owner with all-to-all, deciding there, and returning
 results in the original order gives exactly the decisions of ONE shared
 limiter over the union of the ranks' requests (as the reference's N app
-servers sharing one Redis).  The per-owner decider here is the CPU oracle
-(test infrastructure); on the GPU box it is the HIP engine."""
+servers sharing one Redis).  Here the routing kernels are their CPU
+restatement and the owner's engine is the oracle (test infrastructure); the
+GPU tests (tests/test_route_gpu.py) run the HIP kernels and engine."""
 import os
 import socket
 
@@ -16,79 +17,6 @@ from tracegen import CONFIG_SETS, T0
 CONFIGS = CONFIG_SETS["mixed"]
 
 
-def rank_batches(rank, nbatch=3, m=4000):
-    rng = np.random.default_rng(100 + rank)
-    t = T0
-    out = []
-    for _ in range(nbatch):
-        key = rng.integers(0, 300, m).astype(np.uint64)
-        ts = t + np.cumsum(rng.integers(0, 400_000, m)).astype(np.int64)
-        t = int(ts[-1]) + 1
-        n = rng.choice([1, 1, 2, 5], m).astype(np.int64)
-        cfg = (key % len(CONFIGS)).astype(np.uint32)
-        out.append((key, ts, n, cfg))
-    return out
-
-
-def _worker(rank, world, port, q):
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [root, os.path.join(root, "distributed-rate-limiter_amd", "python"),
-                    os.path.join(root, "tests")]
-    import torch.distributed as dist
-
-    import oracle
-    import shard
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        sim = oracle.OracleSim(0)
-        for a, L, W in CONFIGS:
-            sim.add_config(a, L, W)
-
-        def decide(key, ts, n, cfg):
-            d, r, rt, rs, _ = sim.decide(key, ts, n, cfg)
-            return d, r, rt, rs
-
-        ref = oracle.OracleSim(0)
-        for a, L, W in CONFIGS:
-            ref.add_config(a, L, W)
-        import torch
-
-        def decide_t(key, ts, n, cfg):
-            d, r, rt, rs, _ = sim.decide(key.numpy().view(np.uint64), ts.numpy(), n.numpy(),
-                                         cfg.numpy().view(np.uint32))
-            return (torch.from_numpy(d), torch.from_numpy(r), torch.from_numpy(rt), torch.from_numpy(rs))
-
-        all_batches = [rank_batches(r) for r in range(world)]
-        ok = True
-        for b in range(3):
-            key, ts, n, cfg = all_batches[rank][b]
-            if b % 2 == 0:   # the host (numpy) router
-                got = shard.route_and_decide(key, ts, n, cfg, decide)
-            else:            # the device router (tensors; CPU tensors under gloo here)
-                got = [x.numpy() for x in shard.route_and_decide_torch(
-                    torch.from_numpy(key.view(np.int64)), torch.from_numpy(ts), torch.from_numpy(n),
-                    torch.from_numpy(cfg.view(np.int32)), decide_t)]
-            # expectation: one shared limiter over the union, ordered (ts, rank, pos)
-            parts = [all_batches[r][b] for r in range(world)]
-            U = [np.concatenate([p[f] for p in parts]) for f in range(4)]
-            src = np.concatenate([np.full(p[0].size, r) for r, p in enumerate(parts)])
-            pos = np.concatenate([np.arange(p[0].size) for p in parts])
-            o = np.lexsort((pos, src, U[1]))
-            d, rm, rt, rs, _ = ref.decide(U[0][o], U[1][o], U[2][o], U[3][o])
-            mine = src[o] == rank
-            exp_pos = pos[o][mine]
-            exp = [x[mine] for x in (d, rm, rt, rs)]
-            inv = np.empty_like(exp_pos)
-            inv[exp_pos] = np.arange(exp_pos.size)
-            for g, e in zip(got, exp):
-                ok &= bool(np.array_equal(np.asarray(g, np.int64), np.asarray(e, np.int64)[inv]))
-        q.put((rank, ok))
-    finally:
-        dist.destroy_process_group()
-
-
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -97,33 +25,80 @@ def _free_port():
     return p
 
 
-def test_routed_sharding_matches_single_shared_limiter():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-    assert res == {0: True, 1: True}
-
-
-def test_owner_torch_matches_numpy():
-    import torch
-
-    import shard
-    key = np.random.default_rng(9).integers(0, 1 << 63, 100_000).astype(np.uint64) * np.uint64(2) + np.uint64(1)
-    for world in (2, 3, 8):
-        a = shard.owner_of(key, world)
-        b = shard.owner_of_torch(torch.from_numpy(key.view(np.int64)), world).numpy()
-        assert np.array_equal(a, b)
-
-
 def test_owner_partition_is_balanced():
     import shard
     key = np.arange(1_000_000, dtype=np.uint64)
     for world in (2, 4, 8):
         c = np.bincount(shard.owner_of(key, world), minlength=world)
         assert c.min() > 0.97 * key.size / world
+
+
+# --- the native routed pipeline's orchestration (shard.RoutedPipeline) ---------
+
+def skewed_rank_batches(rank, nbatch=4, m=3000, nkeys=200):
+    """each rank = one app server: its own arrival order, its clock skewed
+    (time goes back across ranks by up to 3 s), some keys shared by all ranks"""
+    rng = np.random.default_rng(300 + rank)
+    t = T0 + [0, -3_000_000_000, 1_200_000_000, -700_000_000][rank % 4]
+    out = []
+    for _ in range(nbatch):
+        key = rng.integers(0, nkeys, m).astype(np.uint64)
+        ts = t + np.cumsum(rng.choice([0, 1, 500, 90_000, 2_000_000], m)).astype(np.int64)
+        ts[rng.random(m) < 0.05] -= 5_000_000   # a few requests out of order within the rank
+        t = int(ts.max()) + 1
+        n = rng.choice([1, 1, 2, 5], m).astype(np.int64)
+        cfg = (key % len(CONFIGS)).astype(np.uint32)
+        out.append((key, ts, n, cfg))
+    return out
+
+
+def _pipeline_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "distributed-rate-limiter_amd", "python"),
+                    os.path.join(root, "tests")]
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    import route_ops
+    import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sim = oracle.OracleSim(0)
+        for a, L, W in CONFIGS:
+            sim.add_config(a, L, W)
+        pg_res = dist.new_group(backend="gloo")
+        pipe = shard.RoutedPipeline(route_ops.NumpyRouteOps(world), route_ops.oracle_decide(sim), world, 4000,
+                                    "cpu", pg_req=None, pg_res=pg_res, depth=4, lookahead=2)
+        all_batches = [skewed_rank_batches(r) for r in range(world)]
+        mine = all_batches[rank]
+        ins = [tuple(torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else
+                                      (x.view(np.int32) if x.dtype == np.uint32 else x)) for x in bt) for bt in mine]
+        outs = [(torch.empty(b[0].size, dtype=torch.uint8),) + tuple(torch.empty(b[0].size, dtype=torch.int64)
+                                                                   for _ in range(3)) for b in mine]
+        pipe.run(ins, outs)
+        exp = route_ops.shared_limiter_expectations(all_batches, rank, CONFIGS)
+        ok = all(np.array_equal(o.numpy().astype(np.int64), np.asarray(e, np.int64))
+                 for ob, eb in zip(outs, exp) for o, e in zip(ob, eb))
+        q.put((rank, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_routed_pipeline_matches_single_shared_limiter():
+    """shard.RoutedPipeline (lookahead count exchange, two process groups,
+    rotating buffer sets) over world size 2 on CPU, with the kernels' CPU
+    restatement and the oracle as the owner's engine: every rank's results
+    equal one shared limiter over the union of the ranks' requests."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == {0: True, 1: True}

@@ -187,6 +187,41 @@ def test_config2_sw_bursty(rl):
     run_both(rl, 0, g.configs, [g.next_batch() for _ in range(4)], tb=1 << 10, win=1 << 22)
 
 
+def test_config2_sw_bursty_full_size(rl):
+    """BASELINE configs[2] at its stated size: 100M keys in an HBM window table
+    of 2^27 entries (8 GiB) + spill, uniform + bursty, 24M requests over 180 s
+    of virtual time (three 60-s windows: previous-window weighting, previous-key
+    expiry and spills of live window keys all occur).  Keys never interact, so
+    the oracle replays a seeded 1/32 sample of the keys (every request of those
+    keys, in order) and must match bit for bit; the whole run is checked by
+    size-independent properties: every request decided, the entries used equal
+    the distinct keys seen, the spill holds window keys."""
+    g = traces.SlidingWindowBursty(nkeys=100_000_000, batch=1_000_000, span_s=180.0, nbatches=24)
+    eng = make_engine(rl, 0, tb=1 << 10, win=1 << 27, max_batch=1 << 20)
+    sim = oracle.OracleSim(0)
+    assert eng.register(*g.configs[0]) == sim.add_config(*g.configs[0])
+    seen = []
+    t_first = None
+    for b in range(24):
+        key, ts, n, cfg = g.next_batch()
+        t_first = t_first if t_first is not None else int(ts[0])
+        res = eng.decide(key, ts, n, cfg, want_tokens=False)
+        assert np.all(res.decision <= 1)
+        pick = (key * np.uint64(0x9E3779B97F4A7C15) >> np.uint64(59)) == np.uint64(0)   # 1/32 of keys
+        ref = sim.decide(key[pick], ts[pick], n[pick], cfg[pick])
+        sub = rl.Decisions(res.decision[pick], res.remaining[pick], res.retry_after_ns[pick],
+                           res.reset_at_ns[pick], None)
+        assert_same(sub, ref, g.configs, cfg[pick], what=f"batch {b}")
+        seen.append(np.unique(key))
+    t_last = int(ts[-1])
+    assert t_last - t_first >= 179 * NS
+    distinct = np.unique(np.concatenate(seen)).size
+    info = eng.table_info(t_last // 1_000_000)
+    assert info.win_used == distinct
+    assert info.spill_used > 0 and info.spill_live > 0
+    eng.close()
+
+
 def test_config3_mixed(rl):
     g = traces.MixedTenants(nkeys=300_000, batch=500_000)
     run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 19, win=1 << 20)
