@@ -9,9 +9,14 @@ A step = one batch through the full engine path (probe/insert into the HBM
 table, radix sort by slot, segment discovery, per-key replay with exact Redis
 Lua "%.14g" semantics), inputs already resident in HBM, results written to HBM.
 
-Multi-GPU (torchrun, one rank per GPU): the key space shards by owner; each
-rank decides its own shard's requests (no data-path collective: the shards
-are independent), so per-GPU work is fixed -> "scaling": "weak".
+Multi-GPU (one rank per GPU; `--gpus N` launches torch.distributed.run itself
+when WORLD_SIZE is unset): BASELINE configs[3] -- mixed per-tenant algorithms
+over 1B keys hash-sharded across the GPUs, every rank taking requests for any
+key, routed to the owner GPU and back by RCCL all-to-alls over xGMI
+(include/rl_route.h, shard.RoutedPipeline).  Per-GPU work is fixed ->
+"scaling": "weak".  The same JSON line carries secondary measurements: the
+metric's Zipf 1M-key workload routed over the same GPUs, and key-shard
+replicas (each rank its own keys, no data-path collective).
 
 Prints one JSON line (rank 0).
 """
@@ -138,63 +143,73 @@ def e2e(args, out_fd):
     os.write(out_fd, (json.dumps(out) + "\n").encode())
 
 
-def main():
-    # one JSON line on stdout: anything native libraries print (the RCCL banner,
-    # ROCm notices) goes to stderr; the line is written to the saved stdout
-    out_fd = os.dup(1)
-    os.dup2(2, 1)
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=4)
-    ap.add_argument("--batch", type=int, default=1_000_000)
-    ap.add_argument("--workload", default="tb_zipf", choices=sorted(WORKLOAD_DESC))
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="cpu_baseline requests per host core")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
-    ap.add_argument("--lat-batches", type=int, default=32,
-                    help="batches of the latency phase (after the timed region): closed loop with the "
-                         "pipeline's depth in flight, per-batch issue->results-complete time")
-    ap.add_argument("--route", action="store_true",
-                    help="routed ingress: every rank draws keys from the whole key space and an RCCL "
-                         "all-to-all moves each request to its owner GPU and the result back")
-    ap.add_argument("--string-keys", action="store_true",
-                    help="requests carry raw string keys ('user:<rank>:<12 hex>'): every step runs the on-GPU "
-                         "FormatKey + XXH64 (rl_hash_keys_device, prefix 'ratelimit') before the decisions")
-    ap.add_argument("--e2e", action="store_true",
-                    help="configs[4]: open-loop Zipf 1.5 traffic through the request coalescer at fixed QPS "
-                         "levels (lib/rl_bench_e2e); reports per-request latency percentiles")
-    ap.add_argument("--qps", default="1e5,1e6,1e7", help="--e2e offered QPS levels")
-    ap.add_argument("--seconds", type=float, default=2.0, help="--e2e seconds per QPS level")
-    args = ap.parse_args()
-    if args.e2e:
-        return e2e(args, out_fd)
+def spawn_ranks(args_list, n, out_fd):
+    """`--gpus N` without a launcher: start torch.distributed.run as a child
+    (before this process touches the GPU) and relay its one JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + args_list
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env)
+    lines = [ln for ln in p.stdout.decode().splitlines() if ln.startswith("{")]
+    if lines:
+        os.write(out_fd, (lines[-1] + "\n").encode())
+    return p.returncode
 
+
+KEYSPACE = {"tb_zipf": (1 << 21, 1024), "tb_zipf15": (1 << 21, 1024), "tb_hot": (1 << 10, 1024),
+            "fw_uniform": (1024, 1 << 15), "sw_bursty": (1024, 1 << 27), "mixed": (1 << 26, 1 << 26)}
+
+
+def roofline_of(eng_stage_ms, nbat, st, algs, uniq, m, workload):
+    per_launch_ms = {
+        "probe": eng_stage_ms[0] / nbat,
+        "sort_pass": eng_stage_ms[1] / nbat / st.sort_passes,
+        "segments": eng_stage_ms[2] / nbat,
+        "replay": eng_stage_ms[3] / nbat,
+        "finish": eng_stage_ms[4] / nbat,
+    }
+    dom = max(per_launch_ms, key=per_launch_ms.get)
+    kname = {"replay": "k_tb_chain<true>", "probe": "k_probe", "sort_pass": "k_sort_pass<false>",
+             "segments": "k_permute", "finish": "k_unpermute"}[dom]
+    # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
+    # passes of this build (scripts/profile.sh: FETCH_SIZE x2 + WRITE_SIZE,
+    # gfx950 correction); `traffic_profile` names the pass
+    traffic, tag = None, None
+    try:
+        tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+        if tj.get("workload", "tb_zipf") == workload and kname in tj["kernels"]:
+            traffic = tj["kernels"][kname]["bytes_per_launch"]
+            tag = tj.get("tag")
+    except (OSError, ValueError, KeyError):
+        pass
+    s_alg = max(STATE_BYTES[a] for a in algs)
+    bytes_per_dec = 24 + 32 + 2 * s_alg * (uniq / m)
+    achieved = bytes_per_dec * m / (per_launch_ms[dom] / 1e3) / 1e9
+    return {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_profile": tag,
+            "algorithmic_bytes_per_launch": bytes_per_dec * m, "bytes_per_decision": bytes_per_dec,
+            "launch_ms": per_launch_ms[dom]}, per_launch_ms
+
+
+def bench_local(args, workload, world, rank, local_rank, dev, sharded):
+    """each rank decides its own batches (N=1: the whole engine; N>1 with
+    `sharded`: each rank owns a disjoint key space -- replicas)"""
     import torch
     import torch.distributed as dist
 
     import rl_amd
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 or args.route:
-        # RCCL over xGMI: barrier + max-over-ranks (sharded), plus the request /
-        # result all-to-alls (routed)
-        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
-            os.environ.setdefault(k, v)
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-
-    gen = make_workload(args.workload, args.batch, rank)
+    gen = make_workload(workload, args.batch, rank)
     nb = args.warmup + args.steps
-    lat_n = 0 if args.route else max(0, args.lat_batches)
+    lat_n = max(0, args.lat_batches) if world == 1 else 0
     host = [gen.next_batch() for _ in range(nb + lat_n)]
-    # sharded ingress: this rank's shard of the key space (ids tagged with the
-    # owner rank); routed ingress: the shared key space, routed per batch
-    tag = np.uint64(0 if args.route else rank) << np.uint64(48)
+    # sharded ingress: this rank's own key space (ids tagged with the rank)
+    tag = np.uint64(rank if sharded else 0) << np.uint64(48)
     uniq = np.unique(host[-1][0]).size
     dev_batches = []
     for key, ts, n, cfg in host:
@@ -219,17 +234,12 @@ def main():
     del host
 
     algs = {a for a, _, _ in gen.configs}
-    need_tb = 1 in algs
-    keyspace = {"tb_zipf": 1 << 21, "tb_zipf15": 1 << 21, "tb_hot": 1 << 10, "fw_uniform": 1 << 15,
-                "sw_bursty": 1 << 27, "mixed": 1 << 26}[args.workload]
-    eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7,
-                        tb_capacity=keyspace if need_tb else 1024,
-                        win_capacity=keyspace if algs - {1} else 1024,
-                        max_batch=args.batch * (2 if args.route else 1), device=local_rank,
+    tb_cap, win_cap = KEYSPACE[workload]
+    eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=tb_cap, win_capacity=win_cap,
+                        max_batch=args.batch, device=local_rank,
                         # inputs are resident before the timed region: batch b+1's
                         # hash/sort/permute overlaps batch b's replay
-                        # (routed: the inputs come out of the all-to-all on torch's stream)
-                        flags=0 if args.no_pipeline or args.route else rl_amd.OPT_PIPELINE)
+                        flags=0 if args.no_pipeline else rl_amd.OPT_PIPELINE)
     for a, L, W in gen.configs:
         eng.register(a, L, W)
     m = args.batch
@@ -245,10 +255,6 @@ def main():
 
     def step(b):
         k, t, n, c = dev_batches[b]
-        if args.route:
-            import shard
-            shard.route_and_decide_torch(k, t, n, c, decide_owned)
-            return
         if args.string_keys:
             # raw keys: hashed on the engine's grouping stream ahead of the probe
             raw, off, _ = key_strings[b]
@@ -262,15 +268,6 @@ def main():
         eng.decide_device(m, k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
                           out_dec.data_ptr(), out_rem.data_ptr(), out_retry.data_ptr(), out_reset.data_ptr(),
                           out_tok.data_ptr(), stream)
-
-    def decide_owned(k, t, n, c):
-        # the owner's merged requests, on this GPU, enqueued on torch's stream
-        mm = k.numel()
-        o = [torch.empty(mm, dtype=torch.uint8, device=dev)] + \
-            [torch.empty(mm, dtype=torch.int64, device=dev) for _ in range(3)]
-        eng.decide_device(mm, k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
-                          *[x.data_ptr() for x in o], 0, torch.cuda.current_stream(dev).cuda_stream)
-        return o
 
     for b in range(args.warmup):
         step(b)
@@ -290,8 +287,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed = time.perf_counter() - t0
     rc = eng.sync()
     if rc != 0:
         raise SystemExit(f"engine error during timed region: {rc} {eng.last_error()}")
@@ -305,8 +301,7 @@ def main():
     # latency runs from the host call to the host seeing its results complete
     # on the caller's stream (an upper bound: batches are waited for in order)
     depth = 1 if args.no_pipeline else 3
-    lat = []
-    pend = []
+    lat, pend = [], []
     for b in range(nb, nb + lat_n):
         if len(pend) >= depth:
             tb, ev = pend.pop(0)
@@ -327,60 +322,22 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-
-    decisions = args.steps * m * world
-    value = decisions / elapsed
-    # per-launch device time of each kernel (HIP events on the launch stream)
-    per_launch_ms = {
-        "probe": stage_ms[0] / nbat,
-        "sort_pass": stage_ms[1] / nbat / st.sort_passes,
-        "segments": stage_ms[2] / nbat,
-        "replay": stage_ms[3] / nbat,
-        "finish": stage_ms[4] / nbat,
-    }
-    dom = max(per_launch_ms, key=per_launch_ms.get)
-    # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
-    # passes (scripts/profile.sh: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction)
-    traffic = None
-    kname = {"replay": "k_tb_chain<true>", "probe": "k_probe", "sort_pass": "k_sort_pass<false>",
-             "segments": "k_permute", "finish": "k_unpermute"}[dom]
-    try:
-        tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
-        if args.workload == "tb_zipf" and kname in tj["kernels"]:
-            traffic = tj["kernels"][kname]["bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        pass
-    s_alg = max(STATE_BYTES[a] for a in algs)
-    bytes_per_dec = 24 + 32 + 2 * s_alg * (uniq / m)
-    achieved = bytes_per_dec * m / (per_launch_ms[dom] / 1e3) / 1e9
+    roof, per_launch_ms = roofline_of(stage_ms, nbat, st, algs, uniq, m, workload)
     latency = None
     if lat:
         la = np.array(lat) * 1e3
         latency = {"p50_batch_ms": float(np.percentile(la, 50)), "p99_batch_ms": float(np.percentile(la, 99)),
                    "max_batch_ms": float(la.max()), "batches": int(la.size), "in_flight": depth,
                    "batch": m, "how": "closed loop after the timed region; host call -> results complete"}
-    out = {
-        "metric": "decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency",
-        "value": value,
-        "unit": "decisions/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+    res = {
+        "value": args.steps * m * world / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64",
-        "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
-        "config": {"workload": WORKLOAD_DESC[args.workload], "batch": m, "unique_keys_per_batch": uniq,
-                   "profile": "redis7 (Lua %.14g state round trip)", "parallelism": (f"routed all-to-all x{world}" if args.route else f"key-shard x{world}"),
-                   "batches_in_flight": 1 if args.no_pipeline or args.route else 3,
-                   "keys": ("raw strings, on-GPU FormatKey + XXH64 in every step" if args.string_keys
-                            else "integer key ids")},
-        "roofline": {"bound": "hbm", "kernel": kname, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "algorithmic_bytes_per_launch": bytes_per_dec * m,
-                     "bytes_per_decision": bytes_per_dec, "launch_ms": per_launch_ms[dom]},
+        "workload": WORKLOAD_DESC[workload],
+        "ingress": "sharded (each rank its own key space, no data-path collective)" if sharded and world > 1
+        else "local",
+        "batch": m, "unique_keys_per_batch": uniq,
+        "batches_in_flight": 1 if args.no_pipeline else 3,
+        "roofline": roof,
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
@@ -388,23 +345,199 @@ def main():
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
                           "replay_timeline_us": {"hot_start": ((int(dbgw[16]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
                                                  "hot_end": ((int(dbgw[17]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
-                                                 "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
-                                                 "stamp_before": ((int(dbgw[18]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100 - (1 << 32) / 100 if dbgw[18] else None,
-                                                 "stamp_after": ((int(dbgw[19]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100 if dbgw[19] else None},
-                          "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]], "near_setup_x16": int(dbgw[39]) * 16,
-                          "hw_id": [hex(int(x)) for x in dbgw[40:45]]},
+                                                 "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100},
+                          "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
+                          "near_setup_x16": int(dbgw[39]) * 16},
         "latency": latency,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
                                                     (stage_ms / nbat).tolist())},
     }
+    eng.close()
+    return res
+
+
+def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
+    """every rank draws requests from the whole key space; the native routed
+    pipeline (include/rl_route.h) moves them to their owners and back"""
+    import torch
+    import torch.distributed as dist
+
+    import rl_amd
+    import shard
+    gen = make_workload(workload, args.batch, rank)
+    nb = args.warmup + args.steps
+    m = args.batch
+    host = [gen.next_batch() for _ in range(nb)]
+    ins = [(torch.from_numpy(k.view(np.int64)).to(dev), torch.from_numpy(t).to(dev), torch.from_numpy(n).to(dev),
+            torch.from_numpy(c.view(np.int32)).to(dev)) for k, t, n, c in host]
+    del host
+    algs = {a for a, _, _ in gen.configs}
+    tb_cap, win_cap = KEYSPACE[workload]
+    eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=tb_cap, win_capacity=win_cap,
+                        max_batch=min(world, 2) * m, device=local_rank, flags=0)
+    for a, L, W in gen.configs:
+        eng.register(a, L, W)
+
+    def decide(mm, key, ts, n, cfg, sms, dec, rem, retry, reset, stream):
+        eng.decide_device(mm, key, ts, n, cfg, sms, dec, rem, retry, reset, None, stream)
+
+    router = rl_amd.Router(local_rank, world, m, world * m)
+    pipe = shard.RoutedPipeline(router, decide, world, m, dev, pg_req=None, pg_res=pg_res)
+    outs = [(torch.empty(m, dtype=torch.uint8, device=dev),) +
+            tuple(torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)) for _ in range(pipe.depth)]
+    recv = []
+    pipe.run(ins[:args.warmup], [outs[b % pipe.depth] for b in range(args.warmup)])
+    torch.cuda.synchronize()
+    for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
+        if rc != 0:
+            raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}")
+    eng.set_timing(True)
+    eng.stage_times()
+    dist.barrier()
+    torch.cuda.synchronize()
+    pipe.wait_s = 0.0
+    t0 = time.perf_counter()
+    pipe.run(ins[args.warmup:], [outs[b % pipe.depth] for b in range(args.steps)],
+             done=lambda b, S: recv.append(pipe.last_recv))
+    t_host = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
+        if rc != 0:
+            raise SystemExit(f"{what} error during timed region: {rc} {eng.last_error()}")
+    stage_ms, nbat = eng.stage_times()
+    st = eng.stats()
+    eng.set_timing(False)
+    tt = torch.tensor([elapsed, float(max(recv)), float(sum(recv))], dtype=torch.float64, device=dev)
+    agg = [torch.zeros_like(tt) for _ in range(world)]
+    dist.all_gather(agg, tt)
+    agg = torch.stack(agg).cpu().numpy()
+    elapsed = float(agg[:, 0].max())
+    mean_recv = float(np.mean(recv))
+    roof, _ = roofline_of(stage_ms, nbat, st, algs, int(st.last_segments), int(round(mean_recv)), workload)
+    res = {
+        "value": args.steps * m * world / elapsed,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "workload": WORKLOAD_DESC[workload],
+        "ingress": f"routed: owner = hash(key) mod {world}, RCCL all-to-all of 32-B request records and "
+                   f"32-B results over xGMI (include/rl_route.h)",
+        "batch": m,
+        "received_per_step": {"mean_over_ranks": float(agg[:, 2].sum() / world / args.steps),
+                              "max_rank_step": float(agg[:, 1].max())},
+        "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
+        "roofline": roof,
+        "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
+                                                    (stage_ms / nbat).tolist())},
+    }
+    eng.close()
+    router.close()
+    return res
+
+
+def main():
+    # one JSON line on stdout: anything native libraries print (the RCCL banner,
+    # ROCm notices) goes to stderr; the line is written to the saved stdout
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=1_000_000)
+    ap.add_argument("--workload", default=None, choices=sorted(WORKLOAD_DESC),
+                    help="default: tb_zipf (configs[1]) on 1 GPU, mixed (configs[3]) on N > 1")
+    ap.add_argument("--ingress", default=None, choices=["routed", "sharded"],
+                    help="N > 1: routed (default; RCCL all-to-all to the key's owner) or sharded (replicas)")
+    ap.add_argument("--no-secondary", action="store_true", help="N > 1: skip the secondary measurements")
+    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="cpu_baseline requests per host core")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
+    ap.add_argument("--lat-batches", type=int, default=32,
+                    help="batches of the latency phase (after the timed region): closed loop with the "
+                         "pipeline's depth in flight, per-batch issue->results-complete time")
+    ap.add_argument("--string-keys", action="store_true",
+                    help="requests carry raw string keys ('user:<rank>:<12 hex>'): every step runs the on-GPU "
+                         "FormatKey + XXH64 (rl_hash_keys_device, prefix 'ratelimit') before the decisions")
+    ap.add_argument("--e2e", action="store_true",
+                    help="configs[4]: open-loop Zipf 1.5 traffic through the request coalescer at fixed QPS "
+                         "levels (lib/rl_bench_e2e); reports per-request latency percentiles")
+    ap.add_argument("--qps", default="1e5,1e6,1e7", help="--e2e offered QPS levels")
+    ap.add_argument("--seconds", type=float, default=2.0, help="--e2e seconds per QPS level")
+    args = ap.parse_args()
+    if args.e2e:
+        return e2e(args, out_fd)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(sys.argv[1:], args.gpus, out_fd)
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    pg_res = None
+    ingress = args.ingress or ("routed" if world > 1 else "local")
+    workload = args.workload or ("mixed" if world > 1 else "tb_zipf")
+    if world > 1 or ingress == "routed":
+        # RCCL over xGMI: the request/count all-to-alls on the default group,
+        # results on a second one (its own stream), barrier and timing
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
+        dist.init_process_group("nccl", device_id=dev)
+        pg_res = dist.new_group(backend="nccl")
+    if ingress == "routed":
+        res = bench_routed(args, workload, world, rank, local_rank, dev, pg_res)
+    else:
+        res = bench_local(args, workload, world, rank, local_rank, dev, sharded=world > 1)
+    secondary = []
+    if world > 1 and not args.no_secondary:
+        # the metric's own workload over the same GPUs, and the replica mode
+        for wl, ing in (("tb_zipf", "routed"), (workload, "sharded")):
+            if (wl, ing) == (workload, ingress):
+                continue
+            r2 = (bench_routed(args, wl, world, rank, local_rank, dev, pg_res) if ing == "routed"
+                  else bench_local(args, wl, world, rank, local_rank, dev, sharded=True))
+            secondary.append({k: r2[k] for k in ("value", "ms_per_step", "workload", "ingress")} |
+                             {"unit": "decisions/s", "roofline_frac": r2["roofline"]["frac"]})
+    out = {
+        "metric": "decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency",
+        "value": res["value"],
+        "unit": "decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": res["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded trace generators, distributed-rate-limiter_amd/python/traces.py)",
+        "config": {"workload": res["workload"], "batch": res["batch"],
+                   "profile": "redis7 (Lua %.14g state round trip)",
+                   "parallelism": res["ingress"] if world > 1 else "1 GPU",
+                   "world_size_seen": world,
+                   "keys": ("raw strings, on-GPU FormatKey + XXH64 in every step" if args.string_keys
+                            else "integer key ids")},
+        "roofline": res["roofline"],
+    }
+    for k in ("unique_keys_per_batch", "batches_in_flight", "received_per_step", "host_ms_per_step"):
+        if k in res:
+            out["config"][k] = res[k]
+    for k in ("replay_detail", "latency", "stages_ms_per_batch"):
+        if k in res:
+            out[k] = res[k]
+    if secondary:
+        out["secondary"] = secondary
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.workload, m, args.cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(workload, args.batch, args.cpu_sample)
     if rank == 0:
         os.write(out_fd, (json.dumps(out) + "\n").encode())
-    eng.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -47,57 +47,96 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_owner(uint32_t m, const uint
 __device__ inline unsigned long long bias(int64_t t) { return (unsigned long long)t ^ 0x8000000000000000ull; }
 __device__ inline int64_t unbias(unsigned long long u) { return (int64_t)(u ^ 0x8000000000000000ull); }
 
-// per-tile owner counts: tile_cnt[tile * world + o]; the batch's latest ts
-// (biased, atomicMax into *maxts)
+// summary of a batch (pack): earliest / latest ts (biased), whether ts ever decreases
+struct PackSum {
+    unsigned long long lo, hi;
+    uint32_t unsorted;
+};
+
+__global__ void k_pack_init(PackSum* sum) { *sum = PackSum{~0ull, 0ull, 0u}; }
+
+// per-tile owner counts: tile_cnt[tile * world + o]; the batch summary
 __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint64_t* __restrict__ key,
                                                          const int64_t* __restrict__ ts, uint32_t world,
-                                                         uint32_t* __restrict__ tile_cnt,
-                                                         unsigned long long* maxts) {
+                                                         uint32_t* __restrict__ tile_cnt, PackSum* sum) {
     __shared__ uint32_t s_cnt[MAX_WORLD];
+    __shared__ uint32_t s_uns;
     if (threadIdx.x < MAX_WORLD) s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_uns = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * RT_TILE;
-    unsigned long long hi = 0;
+    unsigned long long lo = ~0ull, hi = 0;
+    uint32_t uns = 0;
 #pragma unroll
     for (int j = 0; j < RT_ITEMS; j++) {
         const uint32_t i = base + j * RT_BLOCK + threadIdx.x;
         if (i < m) {
             atomicAdd(&s_cnt[owner_of(key[i], world)], 1u);
-            const unsigned long long b = bias(ts[i]);
+            const int64_t t = ts[i];
+            const unsigned long long b = bias(t);
+            lo = b < lo ? b : lo;
             hi = b > hi ? b : hi;
+            if (i > 0 && ts[i - 1] > t) uns = 1;
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long h2 = __shfl_xor(hi, off);
+        const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
         hi = h2 > hi ? h2 : hi;
     }
-    if ((threadIdx.x & 63) == 0 && hi) atomicMax(maxts, hi);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&sum->lo, lo);
+        atomicMax(&sum->hi, hi);
+    }
+    if (uns) s_uns = 1;
     __syncthreads();
+    if (threadIdx.x == 0 && s_uns) atomicOr(&sum->unsorted, 1u);
     if (threadIdx.x < world) tile_cnt[(size_t)blockIdx.x * world + threadIdx.x] = s_cnt[threadIdx.x];
 }
 
-// one block: tile_cnt -> per-(tile, owner) output offsets (in place), the
-// {count, latest ts} pair per owner (int64, for the count all-to-all)
-__global__ void k_route_scan(uint32_t tiles, uint32_t world, uint32_t* __restrict__ tile_cnt,
-                             const unsigned long long* maxts, int64_t* __restrict__ info) {
-    __shared__ uint32_t s_tot[MAX_WORLD];
-    const uint32_t o = threadIdx.x;
-    uint32_t run = 0;
-    if (o < world) {
-        for (uint32_t t = 0; t < tiles; t++) {
-            const uint32_t c = tile_cnt[(size_t)t * world + o];
-            tile_cnt[(size_t)t * world + o] = run;
-            run += c;
-        }
-        s_tot[o] = run;
-        info[2 * o] = run;
-        info[2 * o + 1] = unbias(*maxts);
+// block o: owner o's output offset per tile (the requests of owners before o
+// + an exclusive prefix over tiles) into tile_off, and owner o's info row
+__global__ __launch_bounds__(RT_BLOCK) void k_route_scan(uint32_t tiles, uint32_t world,
+                                                         const uint32_t* __restrict__ tile_cnt,
+                                                         uint32_t* __restrict__ tile_off, const PackSum* sum,
+                                                         int64_t* __restrict__ info) {
+    __shared__ uint32_t s_tmp[RT_BLOCK / 64];
+    __shared__ uint32_t s_run;
+    const uint32_t o = blockIdx.x, tid = threadIdx.x;
+    uint32_t part = 0;
+    for (uint32_t k = tid; k < tiles * o; k += RT_BLOCK) part += tile_cnt[(size_t)(k / o) * world + (k % o)];
+    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
+    if ((tid & 63) == 0) s_tmp[tid >> 6] = part;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t b = 0;
+        for (int w = 0; w < RT_BLOCK / 64; w++) b += s_tmp[w];
+        s_run = b;
     }
     __syncthreads();
-    if (o < world) {
-        uint32_t base = 0;
-        for (uint32_t q = 0; q < o; q++) base += s_tot[q];
-        for (uint32_t t = 0; t < tiles; t++) tile_cnt[(size_t)t * world + o] += base;
+    const uint32_t base = s_run;
+    uint32_t run = base;
+    for (uint32_t t0 = 0; t0 < tiles; t0 += RT_BLOCK) {
+        const uint32_t t = t0 + tid;
+        const uint32_t c = t < tiles ? tile_cnt[(size_t)t * world + o] : 0u;
+        uint32_t inc = wave_incl_scan(c, tid & 63);
+        __syncthreads();
+        if ((tid & 63) == 63) s_tmp[tid >> 6] = inc;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+        for (int w = 0; w < RT_BLOCK / 64; w++) {
+            if (w < (int)(tid >> 6)) pre += s_tmp[w];
+            tot += s_tmp[w];
+        }
+        if (t < tiles) tile_off[(size_t)t * world + o] = run + pre + inc - c;
+        run += tot;
+    }
+    if (tid == 0) {
+        int64_t* row = info + (size_t)RL_ROUTE_INFO * o;
+        row[0] = run - base;
+        row[1] = tiles ? unbias(sum->lo) : INT64_MAX;
+        row[2] = tiles ? unbias(sum->hi) : INT64_MIN;
+        row[3] = sum->unsorted ? 0 : 1;
     }
 }
 
@@ -164,43 +203,21 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(uint32_t m, const ui
     }
 }
 
-// ctrl layout of the merge: [0,1] min ts (biased u64), [2,3] max ts, [4] status,
+// ctrl layout of the merge: [0,1] time-key origin (int64), [2] no sort needed, [4] status,
 // [8 .. 8 + 4*256) digit histograms, then 4 tile counters
-constexpr uint32_t MC_MIN = 0, MC_MAX = 2, MC_STATUS = 4, MC_HIST = 8;
+constexpr uint32_t MC_MIN = 0, MC_IDENT = 2, MC_STATUS = 4, MC_HIST = 8;
 constexpr uint32_t MC_TILE = MC_HIST + MERGE_PASSES * RADIX;
 constexpr uint32_t MC_WORDS = MC_TILE + MERGE_PASSES;
-
-__global__ __launch_bounds__(RT_BLOCK) void k_merge_minmax(uint32_t m, const rl_route_rec* __restrict__ rec,
-                                                           uint32_t* ctrl) {
-    unsigned long long lo = ~0ull, hi = 0ull;
-    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
-        const unsigned long long b = bias(rec[i].ts);
-        lo = b < lo ? b : lo;
-        hi = b > hi ? b : hi;
-    }
-    // wave reduction, then one atomic per wave
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
-        lo = l2 < lo ? l2 : lo;
-        hi = h2 > hi ? h2 : hi;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin((unsigned long long*)(ctrl + MC_MIN), lo);
-        atomicMax((unsigned long long*)(ctrl + MC_MAX), hi);
-    }
-}
 
 // 32-bit time key (ts - min) of every received record + the digit histograms
 // of the four passes
 __global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_route_rec* __restrict__ rec,
                                                          uint32_t* ctrl, uint32_t* __restrict__ kout) {
+    if (ctrl[MC_IDENT]) return;   // no sort: the gather takes the received order
     __shared__ uint32_t lh[MERGE_PASSES][RADIX];
     for (int p = 0; p < MERGE_PASSES; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
-    const int64_t tmin = unbias(*(const unsigned long long*)(ctrl + MC_MIN));
-    const int64_t tmax = unbias(*(const unsigned long long*)(ctrl + MC_MAX));
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (uint64_t)(tmax - tmin) > 0xffffffffull)
-        atomicOr(ctrl + MC_STATUS, RS_SPAN);
+    const int64_t tmin = *(const int64_t*)(ctrl + MC_MIN);
     for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
         const uint32_t k = (uint32_t)(uint64_t)(rec[i].ts - tmin);
         kout[i] = k;
@@ -216,15 +233,17 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_ro
 
 // sorted position p holds received record v[p]: the engine's inputs in
 // order, with the store clock max(floor(ts / 1e6), clock of earlier steps)
-__global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uint32_t* __restrict__ v,
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uint32_t* __restrict__ ctrl,
+                                                           const uint32_t* __restrict__ v,
                                                            const rl_route_rec* __restrict__ rec,
                                                            const int64_t* __restrict__ clock,
                                                            uint64_t* __restrict__ key, int64_t* __restrict__ ts,
                                                            int64_t* __restrict__ n, uint32_t* __restrict__ cfg,
                                                            int64_t* __restrict__ sms, uint32_t* __restrict__ at) {
     const int64_t c0 = *clock;
+    const bool ident = ctrl[MC_IDENT] != 0;
     for (uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x; p < m; p += gridDim.x * RT_BLOCK) {
-        const uint32_t i = v[p];
+        const uint32_t i = ident ? p : v[p];
         const rl_route_rec r = rec[i];
         key[p] = r.key;
         ts[p] = r.ts;
@@ -240,8 +259,9 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uin
 __global__ void k_merge_clock(uint32_t world, const int64_t* __restrict__ info, int64_t* clock) {
     int64_t c = *clock;
     for (uint32_t r = 0; r < world; r++) {
-        if (info[2 * r + 1] == INT64_MIN) continue;   // that rank's batch was empty
-        const int64_t ms = floor_div(info[2 * r + 1], 1000000LL);
+        const int64_t latest = info[(size_t)RL_ROUTE_INFO * r + 2];
+        if (latest == INT64_MIN) continue;   // that rank's batch was empty
+        const int64_t ms = floor_div(latest, 1000000LL);
         c = ms > c ? ms : c;
     }
     *clock = c;
@@ -281,13 +301,14 @@ struct rl_router {
     int device = 0;
     uint32_t world = 1, max_batch = 0, max_recv = 0;
     uint32_t* tile_cnt = nullptr;    // pack: [tiles][world]
+    uint32_t* tile_off = nullptr;    // pack: [tiles][world] output offsets
+    PackSum* psum = nullptr;         // pack: batch summary
     uint32_t* ctrl = nullptr;        // merge: MC_* words + look-back status
     uint32_t* status = nullptr;      // merge: [MERGE_PASSES][tiles][RADIX]
     size_t ctrl_bytes = 0;
     uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr;
     uint32_t* d_status = nullptr;    // sticky router status (RS_*)
     int64_t* clock = nullptr;         // the store clock of the next step (ms)
-    unsigned long long* maxts = nullptr;   // pack: the batch's latest ts (biased)
 };
 
 extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t max_recv,
@@ -306,10 +327,11 @@ extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batc
     const size_t stiles = (max_recv + SORT_TILE - 1) / SORT_TILE;
     r->ctrl_bytes = 4 * (MC_WORDS + (size_t)MERGE_PASSES * stiles * RADIX);
     bool ok = hipMalloc(&r->tile_cnt, 4 * ptiles * world) == hipSuccess;
+    ok = ok && hipMalloc(&r->tile_off, 4 * ptiles * world) == hipSuccess;
+    ok = ok && hipMalloc(&r->psum, sizeof(PackSum)) == hipSuccess;
     ok = ok && hipMalloc(&r->ctrl, r->ctrl_bytes) == hipSuccess;
     for (uint32_t** p : {&r->k0, &r->k1, &r->v0, &r->v1}) ok = ok && hipMalloc(p, 4 * (size_t)max_recv) == hipSuccess;
     ok = ok && hipMalloc(&r->d_status, 4) == hipSuccess && hipMemset(r->d_status, 0, 4) == hipSuccess;
-    ok = ok && hipMalloc(&r->maxts, 8) == hipSuccess;
     if (ok && hipMalloc(&r->clock, 8) == hipSuccess) {
         const int64_t lo = INT64_MIN;
         ok = hipMemcpy(r->clock, &lo, 8, hipMemcpyHostToDevice) == hipSuccess;
@@ -329,7 +351,7 @@ extern "C" int rl_router_destroy(rl_router* r) {
     if (!r) return RL_EINVAL;
     (void)hipSetDevice(r->device);
     for (void* p : {(void*)r->tile_cnt, (void*)r->ctrl, (void*)r->k0, (void*)r->k1, (void*)r->v0, (void*)r->v1,
-                    (void*)r->d_status, (void*)r->clock, (void*)r->maxts})
+                    (void*)r->d_status, (void*)r->clock, (void*)r->tile_off, (void*)r->psum})
         (void)hipFree(p);
     delete r;
     return RL_OK;
@@ -362,19 +384,32 @@ extern "C" int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const 
         return RL_EINVAL;
     (void)hipSetDevice(r->device);
     hipStream_t s = (hipStream_t)stream;
-    // latest ts starts at biased INT64_MIN (0): an empty batch reports INT64_MIN
-    if (hipMemsetAsync(r->maxts, 0, 8, s) != hipSuccess) return RL_EDEVICE;
     const uint32_t tiles = (uint32_t)((m + RT_TILE - 1) / RT_TILE);
-    if (m) k_route_hist<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, r->world, r->tile_cnt, r->maxts);
-    k_route_scan<<<1, MAX_WORLD, 0, s>>>(tiles, r->world, r->tile_cnt, r->maxts, send_info);
+    k_pack_init<<<1, 1, 0, s>>>(r->psum);
+    if (m) k_route_hist<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, r->world, r->tile_cnt, r->psum);
+    k_route_scan<<<r->world, RT_BLOCK, 0, s>>>(tiles, r->world, r->tile_cnt, r->tile_off, r->psum, send_info);
     if (!m) return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
-    k_route_scatter<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, n, cfg, r->world, r->tile_cnt, send, slot);
+    k_route_scatter<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, n, cfg, r->world, r->tile_off, send, slot);
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
 }
 
-__global__ void k_merge_init(uint32_t* ctrl) {
-    *(unsigned long long*)(ctrl + MC_MIN) = ~0ull;
-    *(unsigned long long*)(ctrl + MC_MAX) = 0ull;
+// the merge's plan from the sources' info rows: the time-key origin (earliest
+// ts of any source that sent records), the span check, and whether the
+// received order already is time order (one source, its batch in order)
+__global__ void k_merge_plan(uint32_t world, const int64_t* __restrict__ info, uint32_t* ctrl) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    uint32_t sources = 0, sorted = 1;
+    for (uint32_t r = 0; r < world; r++) {
+        const int64_t* row = info + (size_t)RL_ROUTE_INFO * r;
+        if (row[0] == 0) continue;
+        sources++;
+        sorted &= row[3] != 0;
+        lo = row[1] < lo ? row[1] : lo;
+        hi = row[2] > hi ? row[2] : hi;
+    }
+    *(int64_t*)(ctrl + MC_MIN) = lo;
+    ctrl[MC_IDENT] = sources <= 1 && sorted;
+    if (!ctrl[MC_IDENT] && (uint64_t)(hi - lo) > 0xffffffffull) ctrl[MC_STATUS] |= RS_SPAN;
 }
 
 __global__ void k_merge_status(const uint32_t* ctrl, const uint32_t* sort_flags, uint32_t* status) {
@@ -397,8 +432,7 @@ extern "C" int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* r
     const uint32_t m = (uint32_t)m_recv;
     const uint32_t stiles = (m + SORT_TILE - 1) / SORT_TILE;
     if (hipMemsetAsync(r->ctrl, 0, r->ctrl_bytes, s) != hipSuccess) return RL_EDEVICE;
-    k_merge_init<<<1, 1, 0, s>>>(r->ctrl);
-    k_merge_minmax<<<grid_for(m), RT_BLOCK, 0, s>>>(m, recv, r->ctrl);
+    k_merge_plan<<<1, 1, 0, s>>>(r->world, recv_info, r->ctrl);
     k_merge_keys<<<grid_for(m), RT_BLOCK, 0, s>>>(m, recv, r->ctrl, r->k0);
     // look-back timeouts of the sort land in ctrl[MC_STATUS + 1] (EF_LOOKBACK)
     uint32_t* sflags = r->ctrl + MC_STATUS + 1;
@@ -408,15 +442,15 @@ extern "C" int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* r
         uint32_t* st = r->status + (size_t)p * max_stiles * RADIX;
         if (p == 0)
             k_sort_pass<true><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, r->ctrl + MC_HIST + p * RADIX,
-                                                            st, r->ctrl + MC_TILE + p, sflags);
+                                                            st, r->ctrl + MC_TILE + p, sflags, r->ctrl + MC_IDENT);
         else
             k_sort_pass<false><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p,
                                                              r->ctrl + MC_HIST + p * RADIX, st,
-                                                             r->ctrl + MC_TILE + p, sflags);
+                                                             r->ctrl + MC_TILE + p, sflags, r->ctrl + MC_IDENT);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, vin, recv, r->clock, key, ts, n, cfg, server_ms, at);
+    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, r->ctrl, vin, recv, r->clock, key, ts, n, cfg, server_ms, at);
     k_merge_clock<<<1, 1, 0, s>>>(r->world, recv_info, r->clock);
     k_merge_status<<<1, 1, 0, s>>>(r->ctrl, sflags, r->d_status);
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;

@@ -64,7 +64,9 @@ template <bool FIRST>
 __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, uint32_t m, int shift, const uint32_t* __restrict__ ghist,
-    uint32_t* status, uint32_t* tile_ctr, uint32_t* eflags) {
+    uint32_t* status, uint32_t* tile_ctr, uint32_t* eflags, const uint32_t* skip = nullptr) {
+    // skip (nullable): a device flag that turns the pass into a no-op
+    if (skip && *skip) return;
     __shared__ uint32_t s_wcnt[SORT_WAVES][RADIX];
     __shared__ uint32_t s_goff[RADIX];
     __shared__ uint32_t s_tmp[SORT_WAVES];

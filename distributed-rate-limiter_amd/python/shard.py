@@ -46,6 +46,9 @@ def owner_of(key: np.ndarray, world: int) -> np.ndarray:
 
 # --- the native routed pipeline (include/rl_route.h) ---------------------------
 
+INFO = 4   # RL_ROUTE_INFO
+
+
 def _ctx(stream):
     import contextlib
     return torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
@@ -91,9 +94,10 @@ class RoutedPipeline:
             s = dict(
                 send=torch.empty((mb, 4), dtype=torch.int64, device=d),
                 slot=torch.empty(mb, dtype=torch.int32, device=d),
-                scnt=torch.zeros((world, 2), dtype=torch.int64, device=d),   # {count, latest ts} per owner
-                rcnt=torch.zeros((world, 2), dtype=torch.int64, device=d),   # {count, latest ts} per source
-                cnt_h=torch.zeros((2, world, 2), dtype=torch.int64, pin_memory=self.cuda),
+                # info rows (include/rl_route.h RL_ROUTE_INFO): {count, earliest ts, latest ts, in order}
+                scnt=torch.zeros((world, INFO), dtype=torch.int64, device=d),   # per owner
+                rcnt=torch.zeros((world, INFO), dtype=torch.int64, device=d),   # per source
+                cnt_h=torch.zeros((2, world, INFO), dtype=torch.int64, pin_memory=self.cuda),
                 recv=torch.empty((mr, 4), dtype=torch.int64, device=d),
                 key=torch.empty(mr, dtype=torch.int64, device=d),
                 ts=torch.empty(mr, dtype=torch.int64, device=d),
@@ -112,6 +116,7 @@ class RoutedPipeline:
             )
             self.slots.append(s)
         self.last_recv = 0
+        self.wait_s = 0.0          # host time spent waiting for count copies
 
     @staticmethod
     def _p(t):
@@ -156,7 +161,10 @@ class RoutedPipeline:
         returns the stream on which they are complete"""
         s = self.slots[b % self.depth]
         if s["ev_cnt"] is not None:
+            import time
+            t0 = time.perf_counter()
             s["ev_cnt"].synchronize()
+            self.wait_s += time.perf_counter() - t0
         sc = s["cnt_h"][0][:, 0].tolist()
         rc = s["cnt_h"][1][:, 0].tolist()
         tot, m = int(sum(rc)), s["m"]

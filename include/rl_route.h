@@ -11,7 +11,8 @@
  *
  *   sender   rl_route_pack      owner of every request; requests grouped by
  *                               owner (stable) into 32-byte records; per owner
- *                               {count, the batch's latest ts} (int64 pairs)
+ *                               {count, the batch's earliest and latest ts,
+ *                               whether the batch is in time order} (int64)
  *            all-to-all of the counts, then of the records (RCCL over xGMI;
  *            the caller drives the collectives, e.g. torch.distributed "nccl")
  *   owner    rl_route_merge     the received records -- grouped by source rank,
@@ -79,19 +80,23 @@ int rl_router_sync(rl_router* r, void* stream);
 int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner, void* stream);
 
 /* sender: requests grouped by owner -> send[m] (owner 0's first, each group in
- * batch order); send_info[2 * o] = requests for owner o, send_info[2 * o + 1]
- * = the batch's latest ts (INT64_MIN if empty) -- one int64 pair per owner,
- * exchanged with an equal-split all-to-all; slot[i] = request i's position in
- * send (for rl_route_unpack) */
+ * batch order); send_info[RL_ROUTE_INFO * o + k]: k = 0 requests for owner o,
+ * 1 the batch's earliest ts, 2 its latest ts (INT64_MAX / INT64_MIN if empty),
+ * 3 nonzero when the batch's ts never decrease -- RL_ROUTE_INFO int64 per
+ * owner, exchanged with an equal-split all-to-all; slot[i] = request i's
+ * position in send (for rl_route_unpack) */
+#define RL_ROUTE_INFO 4
 int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
                   const uint32_t* cfg, rl_route_rec* send, int64_t* send_info, uint32_t* slot, void* stream);
 
 /* owner: recv[m_recv] (grouped by source rank) -> the decision order; writes
  * key/ts/n/cfg/server_ms[m_recv] for rl_decide_batch_device and at[i] = the
  * position of received record i in that order.  recv_info: the received
- * send_info pairs (source r's count and latest ts at [2r], [2r + 1]); they
- * advance the store clock after this step.  Call once per step, also when
- * m_recv is 0. */
+ * send_info rows (source r's at [RL_ROUTE_INFO * r]); they bound the time
+ * keys of the merge and advance the store clock after this step.  When only
+ * one source sent records and its batch is in time order, the received order
+ * already is the decision order and no sort runs.  Call once per step, also
+ * when m_recv is 0. */
 int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info, uint64_t* key,
                    int64_t* ts, int64_t* n, uint32_t* cfg, int64_t* server_ms, uint32_t* at, void* stream);
 

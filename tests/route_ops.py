@@ -30,14 +30,17 @@ class NumpyRouteOps:
         rec = np.stack([k.view(np.int64), _arr(ts, m, np.int64), _arr(n, m, np.int64),
                         c | (np.arange(m, dtype=np.int64) << 32)], 1)
         snd[:] = rec[order]
-        info = _arr(scnt, 2 * self.world, np.int64).reshape(self.world, 2)
+        info = _arr(scnt, 4 * self.world, np.int64).reshape(self.world, 4)
+        t = _arr(ts, m, np.int64)
         info[:, 0] = np.bincount(own, minlength=self.world)
-        info[:, 1] = _arr(ts, m, np.int64).max() if m else -(1 << 63)
+        info[:, 1] = t.min() if m else (1 << 63) - 1
+        info[:, 2] = t.max() if m else -(1 << 63)
+        info[:, 3] = int(bool(np.all(t[1:] >= t[:-1])))
         sl = _arr(slot, m, np.int32)
         sl[order] = np.arange(m, dtype=np.int32)
 
     def merge(self, m, recv, info, key, ts, n, cfg, sms, at, stream):
-        latest = _arr(info, 2 * self.world, np.int64).reshape(self.world, 2)[:, 1]
+        latest = _arr(info, 4 * self.world, np.int64).reshape(self.world, 4)[:, 2]
         c0 = self.clock
         live = latest[latest != -(1 << 63)]
         if live.size:

@@ -41,7 +41,7 @@ def test_route_kernels_match_restatement(rl, world):
     r = rl.Router(0, world, m, m)
     k, t, nn, c = _dev_tensors(torch, key, ts, n, cfg)
     send = torch.empty((m, 4), dtype=torch.int64, device="cuda")
-    scnt = torch.empty((world, 2), dtype=torch.int64, device="cuda")
+    scnt = torch.empty((world, 4), dtype=torch.int64, device="cuda")
     slot = torch.empty(m, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     r.pack(m, k.data_ptr(), t.data_ptr(), nn.data_ptr(), c.data_ptr(), send.data_ptr(), scnt.data_ptr(),
@@ -54,7 +54,7 @@ def test_route_kernels_match_restatement(rl, world):
                                                             (x.view(np.int32) if x.dtype == np.uint32 else x)))
                       for x in (key, ts, n, cfg)]
     send_h = torch.empty((m, 4), dtype=torch.int64)
-    scnt_h = torch.empty((world, 2), dtype=torch.int64)
+    scnt_h = torch.empty((world, 4), dtype=torch.int64)
     slot_h = torch.empty(m, dtype=torch.int32)
     ops.pack(m, kc.data_ptr(), tc.data_ptr(), nc.data_ptr(), cc.data_ptr(), send_h.data_ptr(), scnt_h.data_ptr(),
              slot_h.data_ptr(), None)
@@ -64,7 +64,8 @@ def test_route_kernels_match_restatement(rl, world):
     assert torch.equal(scnt.cpu(), scnt_h) and torch.equal(send.cpu(), send_h) and torch.equal(slot.cpu(), slot_h)
     # merge of the packed records (as if received), twice: the second step
     # starts from the store clock the first one left
-    info = torch.tensor([[m // world, int(ts.max()) + r * 2_500_000_000] for r in range(world)], dtype=torch.int64)
+    info = torch.tensor([[m // world, int(ts.min()), int(ts.max()) + r * 100_000_000, 0] for r in range(world)],
+                        dtype=torch.int64)
     for step in range(2):
         outs = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
                [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
@@ -96,6 +97,37 @@ def test_route_kernels_match_restatement(rl, world):
     r.close()
 
 
+def test_merge_single_sorted_source_keeps_order(rl):
+    """one source whose batch is in time order: no sort, the received order
+    is the decision order (and the store clock still advances)"""
+    import torch
+
+    import route_ops
+    m = 9000
+    rng = np.random.default_rng(4)
+    ts = T0 + np.cumsum(rng.integers(0, 5000, m)).astype(np.int64)
+    rec = np.stack([rng.integers(0, 1 << 62, m), ts, np.ones(m, np.int64), np.arange(m, dtype=np.int64) << 32], 1)
+    info = np.array([[m, ts.min(), ts.max(), 1]], np.int64)
+    r = rl.Router(0, 1, m, m)
+    ops = route_ops.NumpyRouteOps(1)
+    s = torch.cuda.current_stream().cuda_stream
+    for step in range(2):
+        d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
+            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
+             torch.empty(m, dtype=torch.int32, device="cuda")]
+        h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
+            [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
+        rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
+        r.merge(m, rt.data_ptr(), it.data_ptr(), *[x.data_ptr() for x in d], s)
+        rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
+        ops.merge(m, rh.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
+        assert r.sync(s) == rl.RL_OK
+        for a, b in zip(d, h):
+            assert torch.equal(a.cpu(), b)
+        assert np.array_equal(d[5].cpu().numpy(), np.arange(m))
+    r.close()
+
+
 def test_merge_reports_a_too_wide_time_span(rl):
     import torch
     m = 5000
@@ -107,7 +139,7 @@ def test_merge_reports_a_too_wide_time_span(rl):
            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
             torch.empty(m, dtype=torch.int32, device="cuda")]
     s = torch.cuda.current_stream().cuda_stream
-    info = torch.tensor([[m, T0]], dtype=torch.int64, device="cuda")
+    info = torch.tensor([[m, T0, T0 + (1 << 33), 0]], dtype=torch.int64, device="cuda")
     r.merge(m, rec.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs], s)
     assert r.sync(s) == rl.RL_EINVAL
     r.close()
