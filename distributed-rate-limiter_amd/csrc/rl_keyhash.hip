@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <string>
 
 #include "../../include/rl_engine.h"
 #include "../../include/rl_keyhash.h"
@@ -262,6 +263,68 @@ extern "C" int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbyt
                                    void* stream) {
     return rl_hash_keys_launch(m, bytes, nbytes, offsets, seed, nullptr, prefix, prefix_len,
                                m ? (double)nbytes / (double)m : 0.0, key_id, stream);
+}
+
+// host XXH64 (the same specification as the device code above)
+static inline uint64_t h_rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t h_round(uint64_t acc, uint64_t in) { return h_rotl(acc + in * P2, 31) * P1; }
+static inline uint64_t h_merge(uint64_t acc, uint64_t v) { return (acc ^ h_round(0, v)) * P1 + P4; }
+static inline uint64_t h_rd64(const uint8_t* p) { uint64_t v; std::memcpy(&v, p, 8); return v; }
+static inline uint32_t h_rd32(const uint8_t* p) { uint32_t v; std::memcpy(&v, p, 4); return v; }
+
+static uint64_t xxh64_host(const uint8_t* p, uint64_t len, uint64_t seed) {
+    uint64_t h, i = 0;
+    if (len >= 32) {
+        uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        for (; i + 32 <= len; i += 32) {
+            v1 = h_round(v1, h_rd64(p + i));
+            v2 = h_round(v2, h_rd64(p + i + 8));
+            v3 = h_round(v3, h_rd64(p + i + 16));
+            v4 = h_round(v4, h_rd64(p + i + 24));
+        }
+        h = h_rotl(v1, 1) + h_rotl(v2, 7) + h_rotl(v3, 12) + h_rotl(v4, 18);
+        h = h_merge(h_merge(h_merge(h_merge(h, v1), v2), v3), v4);
+    } else {
+        h = seed + P5;
+    }
+    h += len;
+    for (; i + 8 <= len; i += 8) h = h_rotl(h ^ h_round(0, h_rd64(p + i)), 27) * P1 + P4;
+    if (i + 4 <= len) {
+        h = h_rotl(h ^ ((uint64_t)h_rd32(p + i) * P1), 23) * P2 + P3;
+        i += 4;
+    }
+    for (; i < len; ++i) h = h_rotl(h ^ ((uint64_t)p[i] * P5), 11) * P1;
+    h ^= h >> 33;
+    h *= P2;
+    h ^= h >> 29;
+    h *= P3;
+    h ^= h >> 32;
+    return h;
+}
+
+extern "C" int rl_hash_keys_host(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
+                                 uint64_t seed, const uint32_t* cfg_id, const char* prefix, size_t prefix_len,
+                                 uint64_t* key_id) {
+    if (prefix_len > RL_KEYHASH_MAX_PREFIX || (prefix_len && !prefix)) return RL_EINVAL;
+    if (m == 0) return RL_OK;
+    if (!offsets || !key_id || (nbytes && !bytes)) return RL_EINVAL;
+    for (size_t i = 0; i < m; ++i)
+        if (offsets[i] > offsets[i + 1]) return RL_EINVAL;
+    if (offsets[m] > nbytes) return RL_EINVAL;
+    std::string buf;
+    if (prefix_len) {
+        buf.assign(prefix, prefix_len);
+        buf.push_back(':');
+    }
+    const size_t plen1 = buf.size();
+    for (size_t i = 0; i < m; ++i) {
+        buf.resize(plen1);
+        buf.append(reinterpret_cast<const char*>(bytes) + offsets[i], offsets[i + 1] - offsets[i]);
+        const uint64_t sd = cfg_id ? RL_CFG_SEED(seed, cfg_id[i]) : seed;
+        const uint64_t h = xxh64_host(reinterpret_cast<const uint8_t*>(buf.data()), buf.size(), sd);
+        key_id[i] = h == RL_KEY_RESERVED ? RL_KEY_RESERVED - 1 : h;
+    }
+    return RL_OK;
 }
 
 extern "C" int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,

@@ -94,6 +94,10 @@ public:
         (void)hipSetDevice(dev_id_);   // the completer thread
         return hipEventSynchronize(dev_[i].ev) == hipSuccess ? RL_OK : RL_EDEVICE;
     }
+    int reset(uint32_t cfg, uint64_t key, int64_t ts) override {
+        (void)hipSetDevice(dev_id_);   // the submitter thread
+        return rl_reset(e_, cfg, key, ts);
+    }
 
 private:
     struct Dev {
@@ -123,7 +127,7 @@ private:
 // synchronous host function (the CPU tests plug the oracle in here)
 class FnBackend : public Backend {
 public:
-    FnBackend(rl_batch_fn fn, void* user) : fn_(fn), user_(user) {}
+    FnBackend(rl_batch_fn fn, rl_reset_fn rfn, void* user) : fn_(fn), rfn_(rfn), user_(user) {}
     int init(int nslots, size_t M, std::vector<Slot>* slots) override {
         slots->resize(nslots);
         mem_.resize(nslots);
@@ -146,16 +150,20 @@ public:
         return fn_(user_, s.m, s.key, s.ts, s.n, s.cfg, s.dec, s.rem, s.retry, s.reset);
     }
     int wait(int, Slot&) override { return RL_OK; }
+    int reset(uint32_t cfg, uint64_t key, int64_t ts) override {
+        return rfn_ ? rfn_(user_, cfg, key, ts) : RL_EINVAL;
+    }
 
 private:
     rl_batch_fn fn_;
+    rl_reset_fn rfn_;
     void* user_;
     std::vector<std::unique_ptr<uint8_t[]>> mem_;
 };
 
 std::unique_ptr<Backend> make_gpu_backend(rl_engine* e) { return std::unique_ptr<Backend>(new GpuBackend(e)); }
-std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, void* user) {
-    return std::unique_ptr<Backend>(new FnBackend(fn, user));
+std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, rl_reset_fn rfn, void* user) {
+    return std::unique_ptr<Backend>(new FnBackend(fn, rfn, user));
 }
 
 // ---------------------------------------------------------------------------
@@ -204,9 +212,10 @@ void Coalescer::Shutdown() {
 }
 
 int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
-                      uint64_t* ticket) {
-    if (!ticket || (m && (!key || !ts || !n || !cfg))) return RL_EINVAL;
+                      uint64_t* ticket, bool reset_op) {
+    if (!ticket || (m && (!key || !ts || !n || !cfg)) || (reset_op && m != 1)) return RL_EINVAL;
     Sub* s = new Sub(m);
+    s->reset_op = reset_op;
     memcpy(s->key, key, 8 * m);
     memcpy(s->ts, ts, 8 * m);
     memcpy(s->n, n, 8 * m);
@@ -284,18 +293,36 @@ void Coalescer::submitter() {
         cv_sub_.wait(lk, [&] { return (stop_ && pending_ == 0) || (pending_ > 0 && inflight_ < (int)o_.max_in_flight); });
         sub_idle_ = false;
         if (pending_ == 0) break;   // stop_ with nothing left
-        if (o_.linger_ns > 0 && inflight_ == 0 && pending_ < o_.max_batch && !stop_) {
+        if (o_.linger_ns > 0 && inflight_ == 0 && pending_ < o_.max_batch && !stop_ && !queue_.front()->reset_op) {
             const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(o_.linger_ns);
             sub_idle_ = true;
             cv_sub_.wait_until(lk, until, [&] { return stop_ || pending_ >= o_.max_batch; });
             sub_idle_ = false;
+        }
+        if (queue_.front()->reset_op) {
+            // every request before it is launched; the backend's reset waits
+            // for them on the device, then applies the DEL
+            Sub* r = queue_.front();
+            queue_.pop_front();
+            pending_ -= 1;
+            r->taken = 1;
+            lk.unlock();
+            const int st = be_->reset(r->cfg[0], r->key[0], r->ts[0]);
+            lk.lock();
+            r->status = st;
+            r->left = 0;
+            r->done = true;
+            r->done_ns = steady_ns();
+            st_.decided += 1;
+            if (r->waiting) r->cv.notify_all();
+            continue;
         }
         const int si = next_slot_;
         next_slot_ = (next_slot_ + 1) % (int)o_.max_in_flight;
         Slot& s = slots_[si];
         s.parts.clear();
         size_t m = 0;
-        while (m < o_.max_batch && !queue_.empty()) {
+        while (m < o_.max_batch && !queue_.empty() && !queue_.front()->reset_op) {
             Sub* sub = queue_.front();
             const size_t take = std::min(sub->m - sub->taken, (size_t)o_.max_batch - m);
             s.parts.push_back({sub, sub->taken, take, m});
@@ -400,7 +427,22 @@ extern "C" int rl_coalescer_create(rl_engine* e, const rl_coalescer_opts* opts, 
 extern "C" int rl_coalescer_create_with_backend(rl_batch_fn fn, void* user, const rl_coalescer_opts* opts,
                                                 rl_coalescer** out) {
     if (!fn || !out) return RL_EINVAL;
-    return create(rlc::make_fn_backend(fn, user), opts, out);
+    return create(rlc::make_fn_backend(fn, nullptr, user), opts, out);
+}
+
+extern "C" int rl_coalescer_create_with_backends(rl_batch_fn fn, rl_reset_fn reset_fn, void* user,
+                                                 const rl_coalescer_opts* opts, rl_coalescer** out) {
+    if (!fn || !out) return RL_EINVAL;
+    return create(rlc::make_fn_backend(fn, reset_fn, user), opts, out);
+}
+
+extern "C" int rl_coalescer_reset(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, uint32_t cfg_id) {
+    if (!c) return RL_EINVAL;
+    uint64_t t;
+    const int64_t one = 1;
+    int rc = c->c->Submit(1, &key_id, &ts_ns, &one, &cfg_id, &t, true);
+    if (rc != RL_OK) return rc;
+    return c->c->Wait(t, -1, nullptr, nullptr, nullptr, nullptr);
 }
 
 extern "C" int rl_coalescer_destroy(rl_coalescer* c) {

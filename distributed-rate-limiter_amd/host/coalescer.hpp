@@ -49,16 +49,20 @@ public:
     virtual int init(int nslots, size_t max_batch, std::vector<Slot>* slots) = 0;
     virtual int launch(int slot, Slot& s) = 0;   // asynchronous
     virtual int wait(int slot, Slot& s) = 0;     // until launch `slot` completed
+    // Reset after every launched batch (the submitter thread; the GPU engine's
+    // rl_reset drains its queues first)
+    virtual int reset(uint32_t cfg, uint64_t key, int64_t ts) = 0;
 };
 
 std::unique_ptr<Backend> make_gpu_backend(rl_engine* e);
-std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, void* user);
+std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, rl_reset_fn rfn, void* user);
 
 // one submission: its requests (copied) and results
 struct Sub {
     uint64_t first = 0;
     size_t m = 0, taken = 0, left = 0;
     int status = RL_OK;
+    bool reset_op = false;        // a Reset (key[0], ts[0], cfg[0]), not requests
     bool done = false;
     bool waiting = false;         // a caller blocks on cv (else completion skips the wake)
     int64_t done_ns = 0;          // steady clock at completion
@@ -79,7 +83,7 @@ public:
     ~Coalescer();
     int start();
     int Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
-               uint64_t* ticket);
+               uint64_t* ticket, bool reset_op = false);
     // done_ns (optional): steady-clock completion time of the submission
     int Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* rem, int64_t* retry, int64_t* reset,
              int64_t* done_ns = nullptr);

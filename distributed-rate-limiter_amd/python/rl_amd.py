@@ -94,6 +94,7 @@ class rl_coalescer_stats(C.Structure):
 vp = C.c_void_p
 # rl_batch_fn (include/rl_coalescer.h)
 BATCH_FN = C.CFUNCTYPE(C.c_int, vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp)
+RESET_FN = C.CFUNCTYPE(C.c_int, vp, C.c_uint32, C.c_uint64, C.c_int64)
 # rll_log_fn (include/rl_limiter.h)
 LOG_FN = C.CFUNCTYPE(None, vp, C.c_int, C.c_char_p, C.c_char_p)
 _sig = {
@@ -137,6 +138,10 @@ _sig = {
     "rll_new_fail_closed_result": (C.c_int, [C.POINTER(rll_result)]),
     "rl_coalescer_create": (C.c_int, [vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_create_with_backend": (C.c_int, [BATCH_FN, vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
+    "rl_coalescer_create_with_backends": (C.c_int, [BATCH_FN, RESET_FN, vp, C.POINTER(rl_coalescer_opts),
+                                                    C.POINTER(vp)]),
+    "rl_coalescer_reset": (C.c_int, [vp, C.c_uint64, C.c_int64, C.c_uint32]),
+    "rl_hash_keys_host": (C.c_int, [C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_char_p, C.c_size_t, vp]),
     "rl_coalescer_destroy": (C.c_int, [vp]),
     "rl_coalescer_submit": (C.c_int, [vp, C.c_size_t, vp, vp, vp, vp, C.POINTER(C.c_uint64)]),
     "rl_coalescer_wait": (C.c_int, [vp, C.c_uint64, C.c_int64, vp, vp, vp, vp]),
@@ -379,6 +384,22 @@ def hash_keys(keys_or_packed, seed: int, prefix: bytes | str = b"", device=0, ch
     return out if check else (rc, out)
 
 
+def hash_keys_host(keys_or_packed, seed: int, prefix: bytes | str = b"", cfg=None) -> np.ndarray:
+    """rl_hash_keys_host: the raw-key ids on the CPU (cfg: per-key config ids
+    mixed into the seed, as rl_decide_batch_keys_device does)."""
+    data, off = keys_or_packed if isinstance(keys_or_packed, tuple) else pack_keys(keys_or_packed)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    pre = prefix.encode() if isinstance(prefix, str) else bytes(prefix)
+    m = len(off) - 1
+    c = None if cfg is None else np.ascontiguousarray(cfg, dtype=np.uint32)
+    out = np.zeros(max(m, 0), dtype=np.uint64)
+    rc = lib.rl_hash_keys_host(m, _ptr(data), data.size, _ptr(off), seed, _ptr(c), pre, len(pre), _ptr(out))
+    if rc != RL_OK:
+        raise EngineError(rc, "rl_hash_keys_host failed")
+    return out
+
+
 def config_validate(algorithm, limit, window_ns):
     """Config.Validate(); algorithm None == nil *Config.  Returns '' or the message."""
     buf = C.create_string_buffer(512)
@@ -532,7 +553,7 @@ class Coalescer:
     the batching logic, a Python function with rl_decide_batch's host-array
     signature (the test seam rl_coalescer_create_with_backend)."""
 
-    def __init__(self, engine, max_batch=65536, max_in_flight=3, linger_ns=0, queue_cap=0):
+    def __init__(self, engine, max_batch=65536, max_in_flight=3, linger_ns=0, queue_cap=0, reset=None):
         o = rl_coalescer_opts(max_batch, max_in_flight, linger_ns, queue_cap)
         h = vp()
         if isinstance(engine, Engine):
@@ -540,7 +561,8 @@ class Coalescer:
             self._fn = None
         else:
             self._fn = BATCH_FN(engine)   # kept alive with the coalescer
-            rc = lib.rl_coalescer_create_with_backend(self._fn, None, C.byref(o), C.byref(h))
+            self._rfn = RESET_FN(reset) if reset else C.cast(None, RESET_FN)
+            rc = lib.rl_coalescer_create_with_backends(self._fn, self._rfn, None, C.byref(o), C.byref(h))
         if rc != RL_OK:
             raise EngineError(rc, "rl_coalescer_create failed")
         self.h = h
@@ -566,6 +588,9 @@ class Coalescer:
         rc = lib.rl_coalescer_decide(self.h, key, ts, n, cfg, C.byref(d), C.byref(rem), C.byref(retry),
                                      C.byref(reset))
         return rc, (d.value, rem.value, retry.value, reset.value)
+
+    def reset(self, key, ts, cfg) -> int:
+        return lib.rl_coalescer_reset(self.h, key, ts, cfg)
 
     def stats(self) -> rl_coalescer_stats:
         st = rl_coalescer_stats()

@@ -63,6 +63,9 @@ typedef int (*rl_batch_fn)(void* user, size_t m, const uint64_t* key_id, const i
                            const int64_t* n, const uint32_t* cfg_id, uint8_t* decision, int64_t* remaining,
                            int64_t* retry_after_ns, int64_t* reset_at_ns);
 
+/* Reset(ctx, key) for the test seam's host backend (rl_reset's signature) */
+typedef int (*rl_reset_fn)(void* user, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns);
+
 /* Coalescer over a GPU engine, on the device current on the calling thread
  * (the engine's: rl_engine_create makes it current).  The engine should be created with
  * RL_OPT_PIPELINE (batch b+1's grouping then overlaps batch b's replay) and
@@ -71,6 +74,9 @@ int rl_coalescer_create(rl_engine* e, const rl_coalescer_opts* opts, rl_coalesce
 /* Test seam: the same coalescer over a synchronous host backend. */
 int rl_coalescer_create_with_backend(rl_batch_fn fn, void* user, const rl_coalescer_opts* opts,
                                      rl_coalescer** out);
+/* ... with Reset too (reset_fn nullable: rl_coalescer_reset then fails with RL_EINVAL) */
+int rl_coalescer_create_with_backends(rl_batch_fn fn, rl_reset_fn reset_fn, void* user,
+                                      const rl_coalescer_opts* opts, rl_coalescer** out);
 /* Completes the queued requests, then stops the threads and frees every
  * submission not yet waited for.  No rl_coalescer_wait may be in progress. */
 int rl_coalescer_destroy(rl_coalescer* c);
@@ -88,6 +94,11 @@ int rl_coalescer_wait(rl_coalescer* c, uint64_t ticket, int64_t timeout_ns, uint
 /* submit(1) + wait: what one Limiter.AllowN call does */
 int rl_coalescer_decide(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, int64_t n, uint32_t cfg_id,
                         uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns);
+/* Reset(ctx, key) at ts_ns (rl_reset, include/rl_engine.h; tokenbucket.go:136-144,
+ * slidingwindow.go:125-139, fixedwindow.go:118-128) in sequence order: after
+ * every request submitted before it, before every request submitted after
+ * it.  Blocks until applied. */
+int rl_coalescer_reset(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, uint32_t cfg_id);
 int rl_coalescer_get_stats(rl_coalescer* c, rl_coalescer_stats* out);
 
 #ifdef __cplusplus

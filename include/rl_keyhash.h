@@ -58,6 +58,13 @@ int rl_hash_keys_device(size_t m, const uint8_t* bytes, uint64_t nbytes, const u
                         uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id,
                         void* stream);
 
+/* The same ids computed on the host CPU (a server's per-request path, where a
+ * GPU launch per key would cost more than the hash): cfg_id nullable -- when
+ * given, request i is hashed with rl_cfg_seed(seed, cfg_id[i]) as
+ * rl_decide_batch_keys_device does.  Offsets as rl_hash_keys. */
+int rl_hash_keys_host(size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets, uint64_t seed,
+                      const uint32_t* cfg_id, const char* prefix, size_t prefix_len, uint64_t* key_id);
+
 /* Host arrays on device `device`: copies in, hashes, copies out.  Synchronous. */
 int rl_hash_keys(int32_t device, size_t m, const uint8_t* bytes, uint64_t nbytes, const uint64_t* offsets,
                  uint64_t seed, const char* prefix, size_t prefix_len, uint64_t* key_id);
