@@ -143,6 +143,49 @@ def e2e(args, out_fd):
     os.write(out_fd, (json.dumps(out) + "\n").encode())
 
 
+def grpc_bench(args, out_fd):
+    """BASELINE configs[4] end to end: the gRPC server (rl_server.py, a child
+    process that owns the GPU) and open-loop gRPC clients (grpc_load.py,
+    Zipf s=1.5 over 1M keys) at fixed offered rates; latency per decision at
+    the client.  This process never touches the GPU."""
+    import subprocess
+    py = os.path.join(ROOT, "distributed-rate-limiter_amd", "python")
+    srv = subprocess.Popen([sys.executable, os.path.join(py, "rl_server.py"), "--address", "127.0.0.1:0",
+                            "--limiter", "default:token_bucket:20:12s", "--tb-capacity", str(1 << 21),
+                            "--win-capacity", "1024"], stdout=subprocess.PIPE)
+    try:
+        line = srv.stdout.readline().decode()
+        if not line.startswith("READY"):
+            raise SystemExit(f"server did not start: {line!r}")
+        addr = f"127.0.0.1:{int(line.split()[1])}"
+        sys.path.insert(0, py)
+        import contextlib
+        import io
+
+        import grpc_load
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            grpc_load.main(["--addr", addr, "--unary", args.grpc_unary, "--batched", args.grpc_batched,
+                            "--seconds", str(args.seconds), "--procs", str(args.grpc_procs)])
+        r = json.loads(buf.getvalue().strip().splitlines()[-1])
+    finally:
+        srv.terminate()
+        srv.wait(60)
+    levels = r["levels"]
+    unary = [lv for lv in levels if lv["batch"] == 1 and lv.get("completed_rpcs") and not lv["errors"]
+             and lv["achieved_decisions_per_s"] >= 0.95 * lv["offered_decisions_per_s"]]
+    top = unary[-1] if unary else levels[0]
+    out = {"metric": "p99 decision latency at fixed offered load through the gRPC server (configs[4])",
+           "value": top.get("p99_us"), "unit": "us", "n_gpus": 1, "higher_is_better": False, "vs_baseline": None,
+           "dtype": "f64", "data": "synthetic (Zipf s=1.5 over 1M keys 'user:<id>', fixed-rate open-loop clients)",
+           "config": {"workload": "configs[4]: gRPC server (api/proto/ratelimiter.proto), Token Bucket 20/12s, "
+                                  "coalesced GPU batches; unary Allow and AllowBatch RPCs",
+                      "value_at": {"rpc_per_s": top.get("offered_rpc_per_s"), "batch": top.get("batch")},
+                      "client_processes": args.grpc_procs, "server": "rl_server.py (grpc sync server, 64 workers)"},
+           "levels": levels}
+    os.write(out_fd, (json.dumps(out) + "\n").encode())
+
+
 def spawn_ranks(args_list, n, out_fd):
     """`--gpus N` without a launcher: start torch.distributed.run as a child
     (before this process touches the GPU) and relay its one JSON line."""
@@ -463,10 +506,17 @@ def main():
                     help="configs[4]: open-loop Zipf 1.5 traffic through the request coalescer at fixed QPS "
                          "levels (lib/rl_bench_e2e); reports per-request latency percentiles")
     ap.add_argument("--qps", default="1e5,1e6,1e7", help="--e2e offered QPS levels")
-    ap.add_argument("--seconds", type=float, default=2.0, help="--e2e seconds per QPS level")
+    ap.add_argument("--seconds", type=float, default=2.0, help="--e2e / --grpc seconds per level")
+    ap.add_argument("--grpc", action="store_true",
+                    help="configs[4] through the gRPC server: open-loop gRPC clients at fixed rates")
+    ap.add_argument("--grpc-unary", default="2000,5000,10000", help="--grpc unary Allow RPC rates")
+    ap.add_argument("--grpc-batched", default="500,2000,4000", help="--grpc AllowBatch (256 per RPC) rates")
+    ap.add_argument("--grpc-procs", type=int, default=6, help="--grpc client processes")
     args = ap.parse_args()
     if args.e2e:
         return e2e(args, out_fd)
+    if args.grpc:
+        return grpc_bench(args, out_fd)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn_ranks(sys.argv[1:], args.gpus, out_fd)
 
