@@ -7,6 +7,9 @@
 
 #include <cstdio>
 #include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
 
 #include "../../include/rl_limiter.h"
 #include "../csrc/rl_semantics.h"
@@ -369,9 +372,45 @@ using namespace ratelimiter;
 struct rll_engine {
     std::unique_ptr<Engine> eng;
 };
+// the LoggingDecorator's records until the caller drains them (pull style:
+// no callback into the caller)
+class LogQueue {
+public:
+    explicit LogQueue(size_t cap) : cap_(cap) {}
+    void push(std::string line) {
+        std::lock_guard<std::mutex> g(mu_);
+        if (q_.size() == cap_) {
+            q_.pop_front();
+            dropped_++;
+        }
+        q_.push_back(std::move(line));
+    }
+    int drain(char* buf, size_t len, uint64_t* dropped) {
+        std::lock_guard<std::mutex> g(mu_);
+        size_t used = 0;
+        int n = 0;
+        while (!q_.empty() && used + q_.front().size() + 1 <= len) {
+            memcpy(buf + used, q_.front().data(), q_.front().size());
+            used += q_.front().size();
+            q_.pop_front();
+            n++;
+        }
+        if (len) buf[used] = '\0';
+        if (dropped) *dropped = dropped_;
+        return n;
+    }
+
+private:
+    std::mutex mu_;
+    std::deque<std::string> q_;
+    size_t cap_;
+    uint64_t dropped_ = 0;
+};
+
 struct rll_limiter {
     std::unique_ptr<RateLimiter> lim;
     MetricsDecorator* metrics = nullptr;   // inside lim, when rll_add_metrics wrapped it
+    std::shared_ptr<LogQueue> logq;        // rll_add_logging's records
 };
 
 static void put_err(char* err, size_t len, const std::string& s) {
@@ -479,16 +518,23 @@ extern "C" int rll_metrics_expose(rll_limiter* l, char* buf, size_t len) {
     return (int)s.size();
 }
 
-extern "C" int rll_add_logging(rll_limiter* l, rll_log_fn fn, void* user) {
-    if (!l || !l->lim || !fn) return RLL_ERR_ARG;
+extern "C" int rll_add_logging(rll_limiter* l, size_t capacity) {
+    if (!l || !l->lim || capacity == 0 || l->logq) return RLL_ERR_ARG;
+    auto q = std::make_shared<LogQueue>(capacity);
+    l->logq = q;
     l->lim.reset(new LoggingDecorator(
         std::move(l->lim),
-        [fn, user](LogLevel lv, const std::string& msg, const std::vector<std::pair<std::string, std::string>>& f) {
+        [q](LogLevel lv, const std::string& msg, const std::vector<std::pair<std::string, std::string>>& f) {
             std::string kv;
             for (const auto& p : f) kv += (kv.empty() ? "" : " ") + p.first + "=" + p.second;
-            fn(user, (int)lv, msg.c_str(), kv.c_str());
+            q->push(std::to_string((int)lv) + "\t" + msg + "\t" + kv + "\n");
         }));
     return RLL_OK;
+}
+
+extern "C" int rll_log_drain(rll_limiter* l, char* buf, size_t len, uint64_t* dropped) {
+    if (!l || !l->logq || (len && !buf)) return -RLL_ERR_ARG;
+    return l->logq->drain(buf, len, dropped);
 }
 
 extern "C" int rll_new_allowed_result(int64_t limit, int64_t remaining, int64_t reset_at_ns, rll_result* out) {

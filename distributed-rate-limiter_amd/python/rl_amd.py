@@ -95,8 +95,6 @@ vp = C.c_void_p
 # rl_batch_fn (include/rl_coalescer.h)
 BATCH_FN = C.CFUNCTYPE(C.c_int, vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp)
 RESET_FN = C.CFUNCTYPE(C.c_int, vp, C.c_uint32, C.c_uint64, C.c_int64)
-# rll_log_fn (include/rl_limiter.h)
-LOG_FN = C.CFUNCTYPE(None, vp, C.c_int, C.c_char_p, C.c_char_p)
 _sig = {
     "rl_engine_create": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp)]),
     "rl_engine_destroy": (C.c_int, [vp]),
@@ -134,7 +132,8 @@ _sig = {
     "rll_new_fail_open_result": (C.c_int, [C.POINTER(rll_result)]),
     "rll_add_metrics": (C.c_int, [vp]),
     "rll_metrics_expose": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
-    "rll_add_logging": (C.c_int, [vp, LOG_FN, vp]),
+    "rll_add_logging": (C.c_int, [vp, C.c_size_t]),
+    "rll_log_drain": (C.c_int, [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint64)]),
     "rll_new_fail_closed_result": (C.c_int, [C.POINTER(rll_result)]),
     "rl_coalescer_create": (C.c_int, [vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_create_with_backend": (C.c_int, [BATCH_FN, vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
@@ -510,11 +509,25 @@ class RateLimiter:
         lib.rll_metrics_expose(self.h, buf, n + 1)
         return buf.value.decode()
 
-    def add_logging(self, sink):
-        """LoggingDecorator (ADR-003): sink(level, msg, fields) per record."""
-        self._log_fn = LOG_FN(lambda u, lv, msg, f: sink(lv, msg.decode(), f.decode()))
-        if lib.rll_add_logging(self.h, self._log_fn, None) != RLL_OK:
+    def add_logging(self, capacity=4096):
+        """LoggingDecorator (ADR-003): records queue in the library until drained."""
+        if lib.rll_add_logging(self.h, capacity) != RLL_OK:
             raise GoError(RLL_ERR_ARG, "rll_add_logging failed")
+
+    def drain_logs(self):
+        """-> ([(level, msg, fields)], dropped)"""
+        out = []
+        dropped = C.c_uint64()
+        while True:
+            buf = C.create_string_buffer(1 << 16)
+            n = lib.rll_log_drain(self.h, buf, 1 << 16, C.byref(dropped))
+            if n < 0:
+                raise GoError(RLL_ERR_ARG, "no logging decorator")
+            for line in buf.value.decode().splitlines():
+                lv, msg, fields = line.split("\t", 2)
+                out.append((int(lv), msg, fields))
+            if n == 0:
+                return out, dropped.value
 
     def reset(self, key, now_ns=NOW_WALL):
         buf = C.create_string_buffer(512)

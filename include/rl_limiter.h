@@ -89,9 +89,15 @@ int rll_allow_batch(rll_limiter* l, size_t m, const char* const* keys, const siz
  * rate_limiter_decision_seconds histogram) and returns its full length. */
 int rll_add_metrics(rll_limiter* l);
 int rll_metrics_expose(rll_limiter* l, char* buf, size_t len);
-/* level: 0 debug, 1 info, 2 warn, 3 error; fields "k=v k=v" */
-typedef void (*rll_log_fn)(void* user, int level, const char* msg, const char* fields);
-int rll_add_logging(rll_limiter* l, rll_log_fn fn, void* user);
+/* LoggingDecorator: records go to a bounded in-library queue that the
+ * caller drains (pull style -- the library never calls back into Go; a full
+ * queue drops its oldest record).  rll_log_drain writes whole records as
+ * text lines "<level>\t<msg>\t<fields>\n" (level: 0 debug, 1 info, 2 warn,
+ * 3 error; fields "k=v k=v") while they fit in buf (NUL-terminated), removes
+ * them from the queue and returns how many it wrote; *dropped (nullable) =
+ * records lost to overflow so far. */
+int rll_add_logging(rll_limiter* l, size_t capacity);
+int rll_log_drain(rll_limiter* l, char* buf, size_t len, uint64_t* dropped);
 
 int rll_reset(rll_limiter* l, const char* key, size_t keylen, int64_t now_ns, char* err, size_t errlen);
 int rll_close(rll_limiter* l);   /* Close(): later calls take the storage-error path */
