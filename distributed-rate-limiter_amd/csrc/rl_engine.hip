@@ -336,7 +336,8 @@ constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iter
                                                // [3..6] round ends (full, stop, partial, first window)
                                                // [8..19] timers [20] exact tiles [21] serial steps
 constexpr uint32_t CTRL_DBGN = 88;
-constexpr uint32_t CTRL_WORDS = CTRL_DBG + CTRL_DBGN;
+constexpr uint32_t CTRL_UPB = CTRL_DBG + CTRL_DBGN;   // [UP_NB] bucket fill counters (k_unpermute_bucket)
+constexpr uint32_t CTRL_WORDS = CTRL_UPB + UP_NB;
 
 uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1;
@@ -379,6 +380,7 @@ struct BatchSet {
     uint32_t* claim = nullptr;
     hipEvent_t front_done = nullptr, chain_done = nullptr, back_done = nullptr;
     uint64_t* kid = nullptr;      // key ids hashed from raw keys (rl_decide_batch_keys_device; lazy)
+    UpRec* upb = nullptr;         // results bucketed by arrival index (k_unpermute_bucket)
     bool used = false;
 };
 
@@ -427,11 +429,13 @@ struct rl_engine {
     hipEvent_t ev_small = nullptr;
     int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
     size_t zero_bytes = 0;
-    int coop_grid = 512;        // k_tb_chain blocks (one per CU fits its LDS)
+    int coop_grid = 96;         // k_tb_chain blocks (one per CU fits its LDS): 96 of 256 CUs, the
+                                // rest run the other batches' grouping and finish (A/B: scripts/ab_grid.sh)
     int probe_grid = 1024;      // k_probe blocks at most
     int perm_grid = 1024;       // k_permute / k_unpermute blocks at most
     uint32_t heavy_min = 32;    // segments this long replay cooperatively
     uint32_t huge_min = 4096;   // token-bucket segments this long are dequeued first
+    bool scatter_unpermute = false;   // RL_SCATTER_UNPERMUTE: the direct-scatter k_unpermute (A/B)
     // dynamic LDS that makes a k_tb_chain block fill its CU's LDS: with two
     // batches in flight, the other batches' grouping and finish kernels (each launched with
     // GROUP_LDS bytes at least) then never share a CU with a chain
@@ -482,6 +486,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.runs.len); (void)hipFree(B.runs.E); (void)hipFree(B.runs.D0); (void)hipFree(B.runs.D1);
     (void)hipFree(B.zero);
     (void)hipFree(B.kid);
+    (void)hipFree(B.upb);
     if (B.front_done) (void)hipEventDestroy(B.front_done);
     if (B.back_done) (void)hipEventDestroy(B.back_done);
     if (B.chain_done) (void)hipEventDestroy(B.chain_done);
@@ -518,6 +523,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.runs.D0, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.runs.D1, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.zero, zero_bytes) == hipSuccess;
+    ok &= hipMalloc(&B.upb, sizeof(UpRec) * std::min<size_t>(M, UP_MAX)) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.front_done, hipEventDisableTiming) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.back_done, hipEventDisableTiming) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.chain_done, hipEventDisableTiming) == hipSuccess;
@@ -656,6 +662,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (const char* v = getenv("RL_PROBE_GRID")) e->probe_grid = atoi(v);
     if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
     e->stamps = getenv("RL_STAMP_KERNELS") != nullptr;
+    e->scatter_unpermute = getenv("RL_SCATTER_UNPERMUTE") != nullptr;
     {
         int dev_lds = 0;
         (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, e->device);
@@ -862,7 +869,15 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (e->timing) (void)hipEventRecord(ev[6], t);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
-    k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
+    if (m <= UP_MAX && !e->scatter_unpermute) {
+        // results to the caller's order through arrival-index buckets: no
+        // scattered partial-line stores
+        k_unpermute_bucket<<<(m + 256 * UP_ITEMS - 1) / (256 * UP_ITEMS), 256, GROUP_LDS, t>>>(
+            kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, B.upb, B.ctrl + CTRL_UPB);
+        k_unpermute_bucket_out<<<(m + UP_BUCKET - 1) / UP_BUCKET, 256, 0, t>>>(m, B.upb, a);
+    } else {
+        k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
+    }
     if (e->timing) {
         (void)hipEventRecord(ev[7], t);
         e->ev_pending.push_back(ev);

@@ -509,4 +509,105 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
     }
 }
 
+// Results to the caller's order without scattered stores (m <= UP_MAX).
+// k_unpermute writes five arrays at random arrival indices: every store is a
+// partial line.  Here (1) k_unpermute_bucket reads the results in sorted
+// order and writes one 40-byte record per request into the bucket of its
+// arrival index (UP_BUCKET consecutive indices; every bucket is full, so
+// bucket b starts at b * UP_BUCKET and a block-aggregated atomic per bucket
+// hands out positions inside it), then (2) k_unpermute_bucket_out places one
+// bucket's records in LDS by arrival index and writes every output array with
+// full-line, coalesced stores.
+constexpr int UP_BUCKET_BITS = 11;
+constexpr uint32_t UP_BUCKET = 1u << UP_BUCKET_BITS;   // arrival indices per bucket
+constexpr uint32_t UP_MAX = 1u << 20;                  // batches up to 2^20: <= 512 buckets
+constexpr uint32_t UP_NB = UP_MAX / UP_BUCKET;
+constexpr int UP_ITEMS = 8;                            // sorted positions per thread (k_unpermute_bucket)
+
+struct alignas(8) UpRec {
+    uint32_t i;        // arrival index
+    uint32_t dec;
+    int64_t rem, retry, reset;
+    double tok;
+};
+
+__global__ __launch_bounds__(256) void k_unpermute_bucket(const uint32_t* __restrict__ sk,
+                                                          const uint32_t* __restrict__ sv, uint32_t m,
+                                                          uint32_t invalid_key, uint32_t win_base,
+                                                          const CfgDev* __restrict__ cfgs, ReqArgs sorted,
+                                                          UpRec* __restrict__ bucketed, uint32_t* bucket_ctr) {
+    __shared__ uint32_t s_cnt[UP_NB], s_base[UP_NB];
+    const uint32_t nb = (m + UP_BUCKET - 1) >> UP_BUCKET_BITS;
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) s_cnt[b] = 0;
+    __syncthreads();
+    const uint32_t j0 = blockIdx.x * (256 * UP_ITEMS);
+    UpRec rec[UP_ITEMS];
+    uint32_t at[UP_ITEMS];
+#pragma unroll
+    for (int q = 0; q < UP_ITEMS; q++) {
+        const uint32_t j = j0 + q * 256 + threadIdx.x;
+        at[q] = 0xffffffffu;
+        if (j >= m) continue;
+        const uint32_t k0 = sk[j];
+        const uint32_t i = sv[j];
+        UpRec r;
+        r.i = i;
+        if (k0 == invalid_key) {   // rejected by k_probe (n <= 0, unknown config or key, table full)
+            r.dec = DEC_INVALID;
+            r.rem = r.retry = r.reset = 0;
+            r.tok = 0.0;
+        } else {
+            const uint8_t dec = sorted.dec[j];
+            r.dec = dec;
+            r.tok = sorted.tok[j];
+            if (k0 < win_base) {
+                tb_result(dec, r.tok, sorted.n[j], cfgs[sorted.cfg[j]], r.rem, r.retry);
+            } else {
+                r.rem = sorted.rem[j];
+                r.retry = sorted.retry[j];
+            }
+            r.reset = sorted.reset[j];
+        }
+        rec[q] = r;
+        at[q] = atomicAdd(&s_cnt[i >> UP_BUCKET_BITS], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += 256)
+        s_base[b] = s_cnt[b] ? atomicAdd(&bucket_ctr[b], s_cnt[b]) : 0u;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < UP_ITEMS; q++) {
+        if (at[q] == 0xffffffffu) continue;
+        const uint32_t b = rec[q].i >> UP_BUCKET_BITS;
+        bucketed[(size_t)b * UP_BUCKET + s_base[b] + at[q]] = rec[q];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_unpermute_bucket_out(uint32_t m, const UpRec* __restrict__ bucketed,
+                                                              ReqArgs out) {
+    __shared__ int64_t s_rem[UP_BUCKET], s_retry[UP_BUCKET], s_reset[UP_BUCKET];
+    __shared__ double s_tok[UP_BUCKET];
+    __shared__ uint8_t s_dec[UP_BUCKET];
+    const uint32_t b = blockIdx.x;
+    const uint32_t base = b * UP_BUCKET;
+    const uint32_t cnt = min(UP_BUCKET, m - base);
+    for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
+        const UpRec r = bucketed[(size_t)base + k];
+        const uint32_t o = r.i - base;
+        s_dec[o] = (uint8_t)r.dec;
+        s_rem[o] = r.rem;
+        s_retry[o] = r.retry;
+        s_reset[o] = r.reset;
+        s_tok[o] = r.tok;
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
+        out.dec[base + k] = s_dec[k];
+        out.rem[base + k] = s_rem[k];
+        out.retry[base + k] = s_retry[k];
+        out.reset[base + k] = s_reset[k];
+        if (out.tok) out.tok[base + k] = s_tok[k];
+    }
+}
+
 }  // namespace rl
