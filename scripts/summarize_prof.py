@@ -67,4 +67,7 @@ for r in stats:
 if traffic:   # a trace-only run (NO_PMC) keeps the last PMC passes' numbers
     # profiles/traffic.json feeds bench.py's roofline: only bench.py profiles write it
     name = "traffic.json" if not os.environ.get("PROF_CMD") else tag + "_traffic.json"
-    json.dump({"tag": tag, "kernels": traffic}, open(os.path.join(dst, name), "w"), indent=1)
+    import subprocess
+    rev = subprocess.run(["git", "-C", root, "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    json.dump({"tag": tag, "workload": os.environ.get("WORKLOAD", "tb_zipf"), "build": rev, "kernels": traffic},
+              open(os.path.join(dst, name), "w"), indent=1)
