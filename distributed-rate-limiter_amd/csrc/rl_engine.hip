@@ -114,7 +114,12 @@ __device__ inline uint32_t probe_request(uint64_t k, uint32_t c, int64_t nn, con
 }
 
 // find-or-insert every request's key; sort key = global slot id; fused
-// per-pass digit histograms (LDS, then one global atomic per bin per block)
+// per-pass digit histograms (LDS, then one global atomic per bin per block).
+// Each thread takes PROBE_R requests and issues their loads phase by phase
+// (inputs, then every first table probe) before resolving any: the kernel is
+// latency-bound on random table reads, and this keeps PROBE_R of them in
+// flight per thread instead of one.
+template <int PROBE_R>
 __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     uint32_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ n,
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
@@ -125,24 +130,54 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
     uint32_t ef = 0;
-    for (uint32_t i = blockIdx.x * PROBE_BLOCK + threadIdx.x; i < m; i += gridDim.x * PROBE_BLOCK) {
-        const uint64_t k = key[i];
-        const uint32_t c = cfg[i];
-        const int64_t nn = n[i];
-        const uint32_t slot = probe_request(k, c, nn, cfgs, ncfg, tb, tb_mask, win, win_mask, win_base,
-                                            invalid_key, ef);
-        sk[i] = slot;
-        // one 32-B record per request: k_permute's sorted-order gather then
-        // touches one line fragment instead of four arrays
-        const int64_t t = a.ts[i];
-        ReqRec r;
-        r.ts = t;
-        r.n = nn;
-        r.sms = a.sms ? a.sms[i] : floor_div(t, 1000000LL);
-        r.cfg = c;
-        r.pad = 0;
-        rec[i] = r;
-        for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
+    for (uint32_t i0 = blockIdx.x * (PROBE_BLOCK * PROBE_R) + threadIdx.x; i0 < m;
+         i0 += gridDim.x * (PROBE_BLOCK * PROBE_R)) {
+        uint64_t k[PROBE_R], h[PROBE_R], cur[PROBE_R];
+        uint32_t c[PROBE_R];
+        int64_t nn[PROBE_R], t[PROBE_R], sms[PROBE_R];
+        bool tbk[PROBE_R], go[PROBE_R];
+#pragma unroll
+        for (int r = 0; r < PROBE_R; r++) {   // inputs
+            const uint32_t i = i0 + r * PROBE_BLOCK;
+            const bool v = i < m;
+            k[r] = v ? key[i] : EMPTY_KEY;
+            c[r] = v ? cfg[i] : 0u;
+            nn[r] = v ? n[i] : 0;
+            t[r] = v ? a.ts[i] : 0;
+            sms[r] = v && a.sms ? a.sms[i] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < PROBE_R; r++) {   // first probes, all in flight
+            const uint32_t i = i0 + r * PROBE_BLOCK;
+            if (i < m && k[r] == EMPTY_KEY) ef |= EF_BAD_KEY;
+            go[r] = i < m && c[r] < ncfg && nn[r] > 0 && k[r] != EMPTY_KEY;
+            tbk[r] = go[r] && cfgs[c[r]].alg == ALG_TOKEN_BUCKET;
+            h[r] = mix64(k[r]) & (tbk[r] ? tb_mask : win_mask);
+            cur[r] = go[r] ? (tbk[r] ? tb[h[r]].key : win[h[r]].key) : EMPTY_KEY;
+        }
+#pragma unroll
+        for (int r = 0; r < PROBE_R; r++) {   // resolve, record, histogram
+            const uint32_t i = i0 + r * PROBE_BLOCK;
+            if (i >= m) continue;
+            uint32_t slot = invalid_key;
+            if (go[r]) {
+                const uint32_t s = tbk[r] ? probe_insert_at(tb, tb_mask, k[r], h[r], cur[r])
+                                          : probe_insert_at(win, win_mask, k[r], h[r], cur[r]);
+                if (s == NO_SLOT) ef |= EF_TABLE_FULL;
+                else slot = tbk[r] ? s : win_base + s;
+            }
+            sk[i] = slot;
+            // one 32-B record per request: k_permute's sorted-order gather then
+            // touches one line fragment instead of four arrays
+            ReqRec q;
+            q.ts = t[r];
+            q.n = nn[r];
+            q.sms = a.sms ? sms[r] : floor_div(t[r], 1000000LL);
+            q.cfg = c[r];
+            q.pad = 0;
+            rec[i] = q;
+            for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
+        }
     }
     if (ef) atomicOr(eflags, ef);
     __syncthreads();
@@ -436,6 +471,7 @@ struct rl_engine {
     uint32_t heavy_min = 32;    // segments this long replay cooperatively
     uint32_t huge_min = 4096;   // token-bucket segments this long are dequeued first
     bool scatter_unpermute = false;   // RL_SCATTER_UNPERMUTE: the direct-scatter k_unpermute (A/B)
+    int probe_r = 1;                  // RL_PROBE_R: requests per k_probe thread (1 or 4; A/B: equal or 1 ahead)
     // dynamic LDS that makes a k_tb_chain block fill its CU's LDS: with two
     // batches in flight, the other batches' grouping and finish kernels (each launched with
     // GROUP_LDS bytes at least) then never share a CU with a chain
@@ -663,6 +699,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
     e->stamps = getenv("RL_STAMP_KERNELS") != nullptr;
     e->scatter_unpermute = getenv("RL_SCATTER_UNPERMUTE") != nullptr;
+    if (const char* v = getenv("RL_PROBE_R")) e->probe_r = atoi(v) == 1 ? 1 : 4;
     {
         int dev_lds = 0;
         (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, e->device);
@@ -809,11 +846,18 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     uint32_t* ghist = B.ctrl + CTRL_HIST;
     // few enough blocks that the per-block histogram flush (3 x 256 global
     // atomics per block on 768 shared words) stays cheap
-    int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, (uint32_t)e->probe_grid);
-    k_probe<<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
-                                                e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
-                                                e->win_base, e->invalid_key, B.sk0, ghist,
-                                                e->sort_passes, a, B.rec, e->d_eflags);
+    const int pr = e->probe_r;
+    int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK * pr - 1) / (PROBE_BLOCK * pr), (uint32_t)e->probe_grid);
+    if (pr == 4)
+        k_probe<4><<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
+                                                       e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
+                                                       e->win_base, e->invalid_key, B.sk0, ghist,
+                                                       e->sort_passes, a, B.rec, e->d_eflags);
+    else
+        k_probe<1><<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
+                                                       e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
+                                                       e->win_base, e->invalid_key, B.sk0, ghist,
+                                                       e->sort_passes, a, B.rec, e->d_eflags);
     if (e->timing) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
@@ -838,10 +882,11 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, B.p_sms, B.o_dec, B.o_rem, B.o_retry, B.o_reset, B.o_tok};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
+    const int pgrid_r = (int)std::min<uint32_t>((m + 256 * PERM_R - 1) / (256 * PERM_R), (uint32_t)e->perm_grid);
     // the TB reset time is state-independent: k_permute writes it straight
     // into the sorted result buffer
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
-    k_permute<<<pgrid, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, B.rec, ps, pre);
+    k_permute<<<pgrid_r, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, B.rec, ps, pre);
     if (e->timing) (void)hipEventRecord(ev[3], f);
     HIPCHK(e, hipEventRecord(B.front_done, f));
 

@@ -408,56 +408,80 @@ struct alignas(32) ReqRec {
 };
 
 // requests to sorted order + the state-free token-bucket precomputation.
-// Each wave covers 64 consecutive sorted positions; a request's predecessor
-// in its segment (position j-1) is the neighbouring lane's record, so only
-// lane 0 gathers a second one.
+// Each wave covers 64 consecutive sorted positions per chunk and PERM_R chunks
+// at once (their sorted-key / index loads, then their record gathers, all in
+// flight before any use: the kernel waits on random gathers); a request's
+// predecessor in its segment (position j-1) is the neighbouring lane's
+// record, so only lane 0 gathers a second one.
+constexpr int PERM_R = 1;   // 4 measured no faster (the gathers are not per-thread latency bound)
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
                                                  const CfgDev* __restrict__ cfgs, int32_t profile,
                                                  const ReqRec* __restrict__ rec, ReqArgs out, TbPre pre) {
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t j0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); j0 < m; j0 += gridDim.x * blockDim.x) {
-        const uint32_t j = j0 + lane;
-        const bool in = j < m;
-        const uint32_t k0 = in ? sk[j] : invalid_key;
-        const bool valid = k0 != invalid_key;
-        ReqRec r{};
-        if (valid) r = rec[sv[j]];
-        // predecessor (j-1) fields from the lane below
-        uint32_t kp = __shfl_up(k0, 1);
-        int64_t tp = __shfl_up(r.ts, 1);
-        int64_t smsp = __shfl_up(r.sms, 1);
-        uint32_t cp = __shfl_up(r.cfg, 1);
-        if (lane == 0) {
-            kp = invalid_key;
-            if (j > 0 && valid && k0 < win_base && sk[j - 1] == k0) {
-                const ReqRec q = rec[sv[j - 1]];
-                kp = k0;
-                tp = q.ts;
-                smsp = q.sms;
-                cp = q.cfg;
+    const uint32_t stride = gridDim.x * blockDim.x * PERM_R;
+    for (uint32_t base = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * PERM_R; base < m; base += stride) {
+        uint32_t k0[PERM_R], kpl[PERM_R], ix[PERM_R], ixp[PERM_R];
+        ReqRec r[PERM_R], q[PERM_R];
+#pragma unroll
+        for (int u = 0; u < PERM_R; u++) {
+            const uint32_t j = base + u * 64 + lane;
+            k0[u] = j < m ? sk[j] : invalid_key;
+            ix[u] = k0[u] != invalid_key ? sv[j] : 0u;
+            // lane 0: the predecessor at j-1 (a previous chunk's last lane)
+            kpl[u] = invalid_key;
+            ixp[u] = 0u;
+            if (lane == 0 && j > 0 && k0[u] != invalid_key && k0[u] < win_base) {
+                kpl[u] = sk[j - 1];
+                if (kpl[u] == k0[u]) ixp[u] = sv[j - 1];
             }
         }
-        if (!valid) continue;
-        // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
-        const_cast<int64_t*>(out.ts)[j] = r.ts;
-        const_cast<int64_t*>(out.n)[j] = r.n;
-        const_cast<uint32_t*>(out.cfg)[j] = r.cfg;
-        const_cast<int64_t*>(out.sms)[j] = r.sms;
-        if (k0 >= win_base) continue;
-        const CfgDev& C = cfgs[r.cfg];
-        const double now = (double)r.ts / 1e9;
-        // state-free: a head's add needs the table (tb_head_add, at replay)
-        // and the table is still being updated by the previous batch
-        if (kp == k0) {
-            const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
-            const int64_t prev_when = expire_when(cfgs[cp].ttl_tb, smsp);
-            pre.add[j] = key_alive(prev_when, r.sms, profile) ? (now - prev_last) * C.rate : __builtin_nan("");
+#pragma unroll
+        for (int u = 0; u < PERM_R; u++) {
+            r[u] = ReqRec{};
+            if (k0[u] != invalid_key) r[u] = rec[ix[u]];
+            if (lane == 0 && kpl[u] == k0[u] && k0[u] != invalid_key) q[u] = rec[ixp[u]];
         }
-        pre.th[j] = fmin(C.limit_d, (double)r.n);
-        pre.reset[j] = tb_reset_at(now, C);
-        pre.lq[j] = lua_tostring_roundtrip(now, profile);
-        pre.when[j] = expire_when(C.ttl_tb, r.sms);
+#pragma unroll
+        for (int u = 0; u < PERM_R; u++) {
+            const uint32_t j = base + u * 64 + lane;
+            const bool valid = k0[u] != invalid_key;
+            // predecessor (j-1) fields from the lane below
+            uint32_t kp = __shfl_up(k0[u], 1);
+            int64_t tp = __shfl_up(r[u].ts, 1);
+            int64_t smsp = __shfl_up(r[u].sms, 1);
+            uint32_t cp = __shfl_up(r[u].cfg, 1);
+            if (lane == 0) {
+                kp = invalid_key;
+                if (kpl[u] == k0[u] && valid) {
+                    kp = k0[u];
+                    tp = q[u].ts;
+                    smsp = q[u].sms;
+                    cp = q[u].cfg;
+                }
+            }
+            if (!valid) continue;
+            // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
+            const_cast<int64_t*>(out.ts)[j] = r[u].ts;
+            const_cast<int64_t*>(out.n)[j] = r[u].n;
+            const_cast<uint32_t*>(out.cfg)[j] = r[u].cfg;
+            const_cast<int64_t*>(out.sms)[j] = r[u].sms;
+            if (k0[u] >= win_base) continue;
+            const CfgDev& C = cfgs[r[u].cfg];
+            const double now = (double)r[u].ts / 1e9;
+            // state-free: a head's add needs the table (tb_head_add, at replay)
+            // and the table is still being updated by the previous batch
+            if (kp == k0[u]) {
+                const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
+                const int64_t prev_when = expire_when(cfgs[cp].ttl_tb, smsp);
+                pre.add[j] = key_alive(prev_when, r[u].sms, profile) ? (now - prev_last) * C.rate
+                                                                     : __builtin_nan("");
+            }
+            pre.th[j] = fmin(C.limit_d, (double)r[u].n);
+            pre.reset[j] = tb_reset_at(now, C);
+            pre.lq[j] = lua_tostring_roundtrip(now, profile);
+            pre.when[j] = expire_when(C.ttl_tb, r[u].sms);
+        }
     }
 }
 

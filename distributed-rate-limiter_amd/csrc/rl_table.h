@@ -83,6 +83,25 @@ __device__ inline uint32_t probe_insert(E* tab, uint64_t mask, uint64_t k) {
     return NO_SLOT;
 }
 
+// probe_insert with the first probe's key word already loaded (`cur`, the
+// key at slot h = mix64(k) & mask): lets a thread issue the first loads of
+// several requests before resolving any (memory-level parallelism)
+template <typename E>
+__device__ inline uint32_t probe_insert_at(E* tab, uint64_t mask, uint64_t k, uint64_t h, uint64_t cur) {
+    const uint64_t lim = mask < MAX_PROBES ? mask : MAX_PROBES;
+    for (uint64_t p = 0; p <= lim; p++) {
+        if (p) cur = tab[h].key;
+        if (cur == k) return (uint32_t)h;
+        if (cur == EMPTY_KEY) {
+            unsigned long long prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY_KEY,
+                                                (unsigned long long)k);
+            if (prev == EMPTY_KEY || prev == k) return (uint32_t)h;
+        }
+        h = (h + 1) & mask;
+    }
+    return NO_SLOT;
+}
+
 // lookup only (Reset path)
 template <typename E>
 __device__ inline uint32_t probe_find(const E* tab, uint64_t mask, uint64_t k) {

@@ -1,10 +1,9 @@
 #!/bin/bash
-# A/B of engine environment knobs: each argument is an env assignment list
-# ("-" = none); runs alternate, twice; prints value and per-stage ms.
+# A/B of engine knobs given as environment assignments, one variant per line
+# of $VARIANTS ("" = default), over $WORKLOADS
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for rep in 1 2; do
-  for v in "$@"; do
-    env $( [ "$v" != "-" ] && echo $v ) timeout -k 10 200 python bench.py --steps ${STEPS:-20} --warmup 3 --lat-batches 0 --no-cpu-baseline ${BARGS:-} \
-      | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', round(d['value']/1e6,1), {k: round(x,4) for k,x in d['stages_ms_per_batch'].items()})" || exit 1
+while IFS= read -r v; do
+  for w in ${WORKLOADS:-tb_zipf mixed}; do
+    env $v TAG="$w [$v]" BARGS="--workload $w --lat-batches 0" STEPS=12 bash scripts/bench_brief.sh | cut -c1-190 || exit 1
   done
-done
+done <<< "${VARIANTS:-}"
