@@ -209,15 +209,12 @@ KEYSPACE = {"tb_zipf": (1 << 21, 1024), "tb_zipf15": (1 << 21, 1024), "tb_hot": 
             "fw_uniform": (1024, 1 << 15), "sw_bursty": (1024, 1 << 27), "mixed": (1 << 26, 1 << 26)}
 
 
-def roofline_of(eng_stage_ms, nbat, st, algs, uniq, m, workload):
-    per_launch_ms = {
-        "probe": eng_stage_ms[0] / nbat,
-        "sort_pass": eng_stage_ms[1] / nbat / st.sort_passes,
-        "segments": eng_stage_ms[2] / nbat,
-        "replay": eng_stage_ms[3] / nbat,
-        "finish": eng_stage_ms[4] / nbat,
-    }
-    dom = max(per_launch_ms, key=per_launch_ms.get)
+def roofline_of(replay_ms, algs, uniq, m, workload):
+    """the dominant kernel is the replay (k_tb_chain: every decision's script
+    replay, the path's critical kernel); its launch time comes from HIP events
+    on its own stream over the timed region"""
+    per_launch_ms = {"replay": replay_ms}
+    dom = "replay"
     kname = {"replay": "k_tb_chain<true>", "probe": "k_probe", "sort_pass": "k_sort_pass<false>",
              "segments": "k_permute", "finish": "k_unpermute"}[dom]
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
@@ -318,7 +315,10 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     rc = eng.sync()
     if rc != 0:
         raise SystemExit(f"engine error during warmup: {rc} {eng.last_error()}")
-    eng.set_timing(True)
+    # timed region: events around the replay only (two per batch on its
+    # stream); the per-stage breakdown comes from the latency phase below
+    timing = 0 if os.environ.get("RL_BENCH_NO_TIMING") else 1
+    eng.set_timing(timing)
     eng.stage_times()  # clear
 
     if world > 1:
@@ -335,9 +335,10 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     if rc != 0:
         raise SystemExit(f"engine error during timed region: {rc} {eng.last_error()}")
     stage_ms, nbat = eng.stage_times()
+    replay_ms = stage_ms[3] / nbat if timing else float("nan")
     st = eng.stats()
     dbgw = eng.debug_words()
-    eng.set_timing(False)
+    eng.set_timing(2)   # every stage, for the breakdown
 
     # latency phase (p99 batch latency of the metric): the next lat_n batches of
     # the same trace, closed loop with `depth` batches in flight; a batch's
@@ -361,11 +362,18 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     rc = eng.sync()
     if rc != 0:
         raise SystemExit(f"engine error during latency phase: {rc} {eng.last_error()}")
+    if lat_n == 0:   # no latency phase: a few untimed batches for the breakdown
+        for b in range(max(0, nb - 4), nb):
+            step(b)
+        torch.cuda.synchronize()
+        eng.sync()
+    stage_ms, nbat = eng.stage_times()
+    eng.set_timing(0)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    roof, per_launch_ms = roofline_of(stage_ms, nbat, st, algs, uniq, m, workload)
+    roof, per_launch_ms = roofline_of(replay_ms, algs, uniq, m, workload)
     latency = None
     if lat:
         la = np.array(lat) * 1e3
@@ -393,7 +401,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "near_setup_x16": int(dbgw[39]) * 16},
         "latency": latency,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
-                                                    (stage_ms / nbat).tolist())},
+                                                    (stage_ms / max(nbat, 1)).tolist())},
+        "stages_how": "HIP events on every stream, over the latency phase (after the timed region, which "
+                      "records events around the replay only)",
     }
     eng.close()
     return res
@@ -434,7 +444,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
         if rc != 0:
             raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}")
-    eng.set_timing(True)
+    eng.set_timing(1)
     eng.stage_times()
     dist.barrier()
     torch.cuda.synchronize()
@@ -451,14 +461,14 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
             raise SystemExit(f"{what} error during timed region: {rc} {eng.last_error()}")
     stage_ms, nbat = eng.stage_times()
     st = eng.stats()
-    eng.set_timing(False)
+    eng.set_timing(0)
     tt = torch.tensor([elapsed, float(max(recv)), float(sum(recv))], dtype=torch.float64, device=dev)
     agg = [torch.zeros_like(tt) for _ in range(world)]
     dist.all_gather(agg, tt)
     agg = torch.stack(agg).cpu().numpy()
     elapsed = float(agg[:, 0].max())
     mean_recv = float(np.mean(recv))
-    roof, _ = roofline_of(stage_ms, nbat, st, algs, int(st.last_segments), int(round(mean_recv)), workload)
+    roof, _ = roofline_of(stage_ms[3] / nbat, algs, int(st.last_segments), int(round(mean_recv)), workload)
     res = {
         "value": args.steps * m * world / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -470,8 +480,6 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
                               "max_rank_step": float(agg[:, 1].max())},
         "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
         "roofline": roof,
-        "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
-                                                    (stage_ms / nbat).tolist())},
     }
     eng.close()
     router.close()

@@ -490,6 +490,7 @@ struct rl_engine {
     // timing: front start, after probe, after sort, after segments+permute
     // (front); replay start, end (chain); finish start, end (tail)
     bool timing = false;
+    bool timing_all = false;    // level 2: every stage; level 1: the replay only (2 events per batch)
     bool stamps = false;        // RL_STAMP_KERNELS: timestamps around each replay (debug words 18, 19)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::array<hipEvent_t, 8>> ev_pending;
@@ -838,9 +839,11 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         a.key = B.kid;
     }
     std::array<hipEvent_t, 8> ev{};
+    const bool tall = e->timing && e->timing_all;   // stage events on every stream
     if (e->timing) {
-        for (auto& x : ev) x = take_event(e);
-        (void)hipEventRecord(ev[0], f);
+        for (int k = 0; k < 8; k++)
+            if (tall || k == 4 || k == 5) ev[k] = take_event(e);
+        if (tall) (void)hipEventRecord(ev[0], f);
     }
     HIPCHK(e, hipMemsetAsync(B.zero, 0, e->zero_bytes, f));
     uint32_t* ghist = B.ctrl + CTRL_HIST;
@@ -858,7 +861,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
                                                        e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
                                                        e->win_base, e->invalid_key, B.sk0, ghist,
                                                        e->sort_passes, a, B.rec, e->d_eflags);
-    if (e->timing) (void)hipEventRecord(ev[1], f);
+    if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
     for (int p = 0; p < e->sort_passes; p++) {
@@ -872,7 +875,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    if (e->timing) (void)hipEventRecord(ev[2], f);
+    if (tall) (void)hipEventRecord(ev[2], f);
     // sorted keys/values are now in kin/vin
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
@@ -887,7 +890,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // into the sorted result buffer
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
     k_permute<<<pgrid_r, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, B.rec, ps, pre);
-    if (e->timing) (void)hipEventRecord(ev[3], f);
+    if (tall) (void)hipEventRecord(ev[3], f);
     HIPCHK(e, hipEventRecord(B.front_done, f));
 
     // replay: after this batch's grouping and the previous replay (stream
@@ -911,7 +914,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     HIPCHK(e, hipEventRecord(B.chain_done, c));
     // finish: outputs of the committed runs, results to the caller's order
     HIPCHK(e, hipStreamWaitEvent(t, B.chain_done, 0));
-    if (e->timing) (void)hipEventRecord(ev[6], t);
+    if (tall) (void)hipEventRecord(ev[6], t);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
     if (m <= UP_MAX && !e->scatter_unpermute) {
@@ -924,7 +927,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     }
     if (e->timing) {
-        (void)hipEventRecord(ev[7], t);
+        if (tall) (void)hipEventRecord(ev[7], t);
         e->ev_pending.push_back(ev);
     }
     HIPCHK(e, hipEventRecord(B.back_done, t));
@@ -1178,6 +1181,7 @@ extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
 extern "C" int rl_engine_set_timing(rl_engine* e, int on) {
     if (!e) return RL_EINVAL;
     e->timing = on != 0;
+    e->timing_all = on != 1;   // 1: replay events only
     return RL_OK;
 }
 
@@ -1185,15 +1189,17 @@ extern "C" int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint
     if (!e) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     for (auto& ev : e->ev_pending) {
-        HIPCHK(e, hipEventSynchronize(ev[7]));
+        HIPCHK(e, hipEventSynchronize(ev[7] ? ev[7] : ev[5]));
         static const int from[NSTAGES] = {0, 1, 2, 4, 6}, to[NSTAGES] = {1, 2, 3, 5, 7};
         for (int k = 0; k < NSTAGES; k++) {
+            if (!ev[from[k]] || !ev[to[k]]) continue;
             float t = 0;
             HIPCHK(e, hipEventElapsedTime(&t, ev[from[k]], ev[to[k]]));
             e->stage_ms[k] += t;
         }
         e->timed_batches++;
-        for (auto x : ev) e->ev_pool.push_back(x);
+        for (auto x : ev)
+            if (x) e->ev_pool.push_back(x);
     }
     e->ev_pending.clear();
     for (int k = 0; k < nstages && k < NSTAGES; k++) ms[k] = e->stage_ms[k];

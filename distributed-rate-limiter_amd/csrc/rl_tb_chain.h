@@ -407,7 +407,19 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     const uint32_t myoff = toff + lane * K;
     const uint32_t nv = myoff < pcnt ? ((pcnt - myoff) < (uint32_t)K ? (pcnt - myoff) : (uint32_t)K) : 0u;
     const uint32_t i0 = pfirst + myoff;
-    const double lim = 0.5 - (2.0 * dmax * 0x1.0000001p-53 + 0x1p-40);
+    // near band: a step is far when |frac(add P)| + |delta| < 1/2, with
+    // delta = (eta + eps) P the rounding errors of x = strtod(D) and of
+    // sum = x + add, |eta|, |eps| <= ulp / 2.  Every state is <= dmax, so x and
+    // sum are <= dmax / P = f 2^e (f in [1/2, 1)) and their ulp <= 2^(e - 53):
+    // |delta| <= 2^(e - 53) P -- the binade bound, up to 2x tighter than
+    // (|D| + |D'|) 2^-53 (which the binary mode keeps)
+    double band = 2.0 * dmax * 0x1.0000001p-53;
+    if (MODE == QM_DEC) {
+        int e;
+        (void)frexp(dmax / P * 0x1.0000001p+0, &e);
+        band = ldexp(P, e - 53) * 0x1.0000001p+0;
+    }
+    const double lim = 0.5 - (band + 0x1p-40);
     const double PY = P * CH_YSCALE;
     double add[K], th[K], cb[K];
     double cum = 0.0, ymin = __builtin_inf(), cmax = -__builtin_inf(), cmin = __builtin_inf();

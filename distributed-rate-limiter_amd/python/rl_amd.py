@@ -287,8 +287,9 @@ class Engine:
             raise EngineError(rc, self.last_error())
         return rc, out
 
-    def set_timing(self, on: bool):
-        lib.rl_engine_set_timing(self.h, 1 if on else 0)
+    def set_timing(self, level):
+        """0 off, 1 replay events only (timed runs), 2 every stage (True == 2)"""
+        lib.rl_engine_set_timing(self.h, 2 if level is True else int(level))
 
     def stage_times(self):
         ms = np.zeros(5, np.float64)

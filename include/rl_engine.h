@@ -159,7 +159,9 @@ int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, uint64_t win
 /* per-stage device time (ms) accumulated since the last call, measured with
  * HIP events on the stream the kernels run on; stages: 0 probe, 1 sort,
  * 2 segments + permute, 3 replay (k_tb_chain), 4 finish (run expansion +
- * unpermute).  Requires rl_engine_set_timing(e, 1). */
+ * unpermute).  rl_engine_set_timing(e, on): 0 off, 1 the replay only (two
+ * events per batch on its stream: what a timed benchmark can afford), 2 every
+ * stage. */
 int rl_engine_set_timing(rl_engine* e, int on);
 int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint64_t* batches);
 /* diagnostic: the last batch's replay debug counters (up to 88 words; layout in rl_engine.hip CTRL_DBG) */
