@@ -247,7 +247,8 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     gen = make_workload(workload, args.batch, rank)
     nb = args.warmup + args.steps
     lat_n = max(0, args.lat_batches) if world == 1 else 0
-    host = [gen.next_batch() for _ in range(nb + lat_n)]
+    extra = lat_n if lat_n else 4      # batches after the timed region (latency / stage breakdown)
+    host = [gen.next_batch() for _ in range(nb + extra)]
     # sharded ingress: this rank's own key space (ids tagged with the rank)
     tag = np.uint64(rank if sharded else 0) << np.uint64(48)
     uniq = np.unique(host[-1][0]).size
@@ -338,6 +339,18 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     replay_ms = stage_ms[3] / nbat if timing else float("nan")
     st = eng.stats()
     dbgw = eng.debug_words()
+    stamp_ring = None
+    if os.environ.get("RL_STAMP_KERNELS"):
+        sr = eng.debug_stamps()
+        if sr is not None:
+            first = (st.batches - args.steps) % 256   # slots of the timed batches
+            rows = np.array([sr[(first + i) % 256] for i in range(min(args.steps, 256))], np.int64)
+            rel = (rows - rows[0, 0]) & 0xffffffff
+            us = rel / 100.0
+            stamp_ring = {"per_batch_us [front0, front1, replay0, replay1, finish0, finish1]": us.round(1).tolist(),
+                          "replay_us_mean": float(np.mean(us[:, 3] - us[:, 2])),
+                          "replay_period_us_mean": float(np.mean(np.diff(us[:, 2]))) if len(us) > 1 else None,
+                          "front_us_mean": float(np.mean(us[:, 1] - us[:, 0]))}
     eng.set_timing(2)   # every stage, for the breakdown
 
     # latency phase (p99 batch latency of the metric): the next lat_n batches of
@@ -362,8 +375,8 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     rc = eng.sync()
     if rc != 0:
         raise SystemExit(f"engine error during latency phase: {rc} {eng.last_error()}")
-    if lat_n == 0:   # no latency phase: a few untimed batches for the breakdown
-        for b in range(max(0, nb - 4), nb):
+    if lat_n == 0:   # no latency phase: the next few batches of the trace for the breakdown
+        for b in range(nb, nb + extra):
             step(b)
         torch.cuda.synchronize()
         eng.sync()
@@ -396,10 +409,14 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
                           "replay_timeline_us": {"hot_start": ((int(dbgw[16]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
                                                  "hot_end": ((int(dbgw[17]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
-                                                 "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100},
+                                                 "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
+                                                 # RL_STAMP_KERNELS=1: one-lane kernels just before / after the replay on its stream
+                                                 "stamp_before": (((int(dbgw[18]) - (~int(dbgw[13]) & 0xffffffff) + (1 << 31)) & 0xffffffff) - (1 << 31)) / 100 if dbgw[18] else None,
+                                                 "stamp_after": (((int(dbgw[19]) - (~int(dbgw[13]) & 0xffffffff) + (1 << 31)) & 0xffffffff) - (1 << 31)) / 100 if dbgw[19] else None},
                           "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
                           "near_setup_x16": int(dbgw[39]) * 16},
         "latency": latency,
+        "stamp_ring": stamp_ring,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
                                                     (stage_ms / max(nbat, 1)).tolist())},
         "stages_how": "HIP events on every stream, over the latency phase (after the timed region, which "
@@ -584,8 +601,8 @@ def main():
     for k in ("unique_keys_per_batch", "batches_in_flight", "received_per_step", "host_ms_per_step"):
         if k in res:
             out["config"][k] = res[k]
-    for k in ("replay_detail", "latency", "stages_ms_per_batch"):
-        if k in res:
+    for k in ("replay_detail", "latency", "stages_ms_per_batch", "stamp_ring"):
+        if res.get(k) is not None:
             out[k] = res[k]
     if secondary:
         out["secondary"] = secondary

@@ -361,6 +361,7 @@ __global__ void k_q14(const double* in, double* out, uint32_t n) {
 namespace {
 
 constexpr int NSTAGES = 5;
+constexpr uint32_t STAMP_RING = 256;
 constexpr int NSETS = 3;          // batch buffer sets: grouping b+1 | replay b | finish b-1
 constexpr int GROUP_LDS = 4096;   // LDS floor of the grouping / finish kernels (see rl_engine::chain_pad)
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
@@ -477,6 +478,7 @@ struct rl_engine {
     // GROUP_LDS bytes at least) then never share a CU with a chain
     size_t chain_pad[2] = {0, 0};
     uint32_t* d_eflags = nullptr;
+    uint32_t* stamp_ring = nullptr;   // RL_STAMP_KERNELS diagnostics
 
     // host-API staging (device side)
     uint64_t* d_key = nullptr;
@@ -561,9 +563,13 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.runs.D1, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.zero, zero_bytes) == hipSuccess;
     ok &= hipMalloc(&B.upb, sizeof(UpRec) * std::min<size_t>(M, UP_MAX)) == hipSuccess;
-    ok &= hipEventCreateWithFlags(&B.front_done, hipEventDisableTiming) == hipSuccess;
+    // front_done / chain_done only order the engine's own streams on this
+    // device: a device-scope release (no system-scope cache writeback per
+    // batch); back_done hands results to the caller and keeps the default
+    const unsigned inner = hipEventDisableTiming | (getenv("RL_EV_SYSFENCE") ? 0u : hipEventReleaseToDevice);
+    ok &= hipEventCreateWithFlags(&B.front_done, inner) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.back_done, hipEventDisableTiming) == hipSuccess;
-    ok &= hipEventCreateWithFlags(&B.chain_done, hipEventDisableTiming) == hipSuccess;
+    ok &= hipEventCreateWithFlags(&B.chain_done, inner) == hipSuccess;
     if (!ok) return false;
     B.ctrl = B.zero;
     B.status = B.zero + CTRL_WORDS;
@@ -579,6 +585,7 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_spill);
     for (auto& B : e->set) free_set(B);
     (void)hipFree(e->d_eflags);
+    (void)hipFree(e->stamp_ring);
     (void)hipFree(e->small_kid);
     (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
     (void)hipFree(e->d_dec); (void)hipFree(e->d_rem); (void)hipFree(e->d_retry); (void)hipFree(e->d_reset); (void)hipFree(e->d_tok);
@@ -699,6 +706,10 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (const char* v = getenv("RL_PROBE_GRID")) e->probe_grid = atoi(v);
     if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
     e->stamps = getenv("RL_STAMP_KERNELS") != nullptr;
+    if (e->stamps) {
+        if (hipMalloc(&e->stamp_ring, 4 * 6 * STAMP_RING) != hipSuccess) return bail(RL_ENOMEM);
+        if (hipMemset(e->stamp_ring, 0, 4 * 6 * STAMP_RING) != hipSuccess) return bail(RL_EDEVICE);
+    }
     e->scatter_unpermute = getenv("RL_SCATTER_UNPERMUTE") != nullptr;
     if (const char* v = getenv("RL_PROBE_R")) e->probe_r = atoi(v) == 1 ? 1 : 4;
     {
@@ -767,8 +778,9 @@ static hipEvent_t take_event(rl_engine* e) {
         e->ev_pool.pop_back();
         return ev;
     }
+    // timestamps only: a device-scope release
     hipEvent_t ev;
-    (void)hipEventCreate(&ev);
+    (void)hipEventCreateWithFlags(&ev, getenv("RL_EV_SYSFENCE") ? 0u : hipEventReleaseToDevice);
     return ev;
 }
 
@@ -845,6 +857,10 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
             if (tall || k == 4 || k == 5) ev[k] = take_event(e);
         if (tall) (void)hipEventRecord(ev[0], f);
     }
+    // diagnostic stamp ring (RL_STAMP_KERNELS): per batch the realtime of
+    // front start / end, replay start / end, finish start / end
+    uint32_t* sr = e->stamp_ring ? e->stamp_ring + 6 * (e->stats.batches % STAMP_RING) : nullptr;
+    if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 0);
     HIPCHK(e, hipMemsetAsync(B.zero, 0, e->zero_bytes, f));
     uint32_t* ghist = B.ctrl + CTRL_HIST;
     // few enough blocks that the per-block histogram flush (3 x 256 global
@@ -891,6 +907,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
     k_permute<<<pgrid_r, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, B.rec, ps, pre);
     if (tall) (void)hipEventRecord(ev[3], f);
+    if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 1);
     HIPCHK(e, hipEventRecord(B.front_done, f));
 
     // replay: after this batch's grouping and the previous replay (stream
@@ -899,6 +916,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     HIPCHK(e, hipStreamWaitEvent(c, B.front_done, 0));
     if (e->timing) (void)hipEventRecord(ev[4], c);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 18);
+    if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 2);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
     if (ncfg <= (uint32_t)MAX_LCFG)
@@ -910,11 +928,13 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
                                                             e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
                                                             B.runs);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 19);
+    if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 3);
     if (e->timing) (void)hipEventRecord(ev[5], c);
     HIPCHK(e, hipEventRecord(B.chain_done, c));
     // finish: outputs of the committed runs, results to the caller's order
     HIPCHK(e, hipStreamWaitEvent(t, B.chain_done, 0));
     if (tall) (void)hipEventRecord(ev[6], t);
+    if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 4);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
     if (m <= UP_MAX && !e->scatter_unpermute) {
@@ -926,6 +946,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     } else {
         k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
     }
+    if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 5);
     if (e->timing) {
         if (tall) (void)hipEventRecord(ev[7], t);
         e->ev_pending.push_back(ev);
@@ -1206,6 +1227,19 @@ extern "C" int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint
     if (batches) *batches = e->timed_batches;
     for (int k = 0; k < NSTAGES; k++) e->stage_ms[k] = 0;
     e->timed_batches = 0;
+    return RL_OK;
+}
+
+// diagnostic (RL_STAMP_KERNELS=1): the stamp ring, 6 words per batch
+// (realtime, 10 ns) for batches b mod STAMP_RING
+extern "C" int rl_engine_debug_stamps(rl_engine* e, uint32_t* out, size_t n) {
+    if (!e || !out) return RL_EINVAL;
+    if (!e->stamp_ring) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    if (n > 6 * STAMP_RING) n = 6 * STAMP_RING;
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    HIPCHK(e, hipMemcpy(out, e->stamp_ring, 4 * n, hipMemcpyDeviceToHost));
     return RL_OK;
 }
 

@@ -110,6 +110,7 @@ _sig = {
     "rl_engine_stage_times": (C.c_int, [vp, vp, C.c_int, C.POINTER(C.c_uint64)]),
     "rl_last_error": (C.c_int, [vp, C.c_char_p, C.c_size_t]),
     "rl_engine_debug_words": (C.c_int, [vp, vp, C.c_size_t]),
+    "rl_engine_debug_stamps": (C.c_int, [vp, vp, C.c_size_t]),
     "rl_selftest_q14_host": (C.c_int, [vp, vp, C.c_size_t]),
     "rl_selftest_q14_device": (C.c_int, [vp, vp, vp, C.c_size_t]),
     "rll_engine_new": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp), C.c_char_p, C.c_size_t]),
@@ -267,6 +268,14 @@ class Engine:
         s = rl_stats()
         lib.rl_engine_stats(self.h, C.byref(s))
         return s
+
+    def debug_stamps(self) -> np.ndarray | None:
+        """RL_STAMP_KERNELS=1 diagnostics: [256, 6] realtime (10 ns) stamps per
+        batch slot (front start/end, replay start/end, finish start/end)"""
+        out = np.zeros(6 * 256, np.uint32)
+        if lib.rl_engine_debug_stamps(self.h, _ptr(out), out.size) != 0:
+            return None
+        return out.reshape(256, 6)
 
     def debug_words(self, n=88) -> np.ndarray:
         out = np.zeros(n, np.uint32)
