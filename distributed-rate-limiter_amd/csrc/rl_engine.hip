@@ -1243,6 +1243,18 @@ extern "C" int rl_engine_debug_stamps(rl_engine* e, uint32_t* out, size_t n) {
     return RL_OK;
 }
 
+// diagnostic: device calls of the q14 big-integer slow paths so far
+extern "C" int rl_engine_debug_q14_slow(rl_engine* e, uint64_t* out) {
+    if (!e || !out) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    unsigned long long v = 0;
+    HIPCHK(e, hipMemcpyFromSymbol(&v, HIP_SYMBOL(rlq::q14_slow_calls), sizeof v, 0, hipMemcpyDeviceToHost));
+    *out = v;
+    return RL_OK;
+}
+
 // diagnostic: the last batch's replay debug words (include/rl_engine.h)
 extern "C" int rl_engine_debug_words(rl_engine* e, uint32_t* out, size_t n) {
     if (!e || !out) return RL_EINVAL;

@@ -38,6 +38,18 @@
 
 namespace rlq {
 
+#if defined(__HIPCC__)
+// diagnostic: device calls of the big-integer slow paths (each costs
+// hundreds of microseconds to milliseconds of one lane); read by
+// rl_engine_debug_q14_slow
+static __device__ unsigned long long q14_slow_calls;
+#define RL_COUNT_SLOW() atomicAdd(&q14_slow_calls, 1ull)
+#endif
+#if !defined(__HIP_DEVICE_COMPILE__)
+#undef RL_COUNT_SLOW
+#define RL_COUNT_SLOW() ((void)0)
+#endif
+
 // 10^k, k in [0,22]: every partial product is a power of ten <= 1e22, hence exact.
 RL_INLINE double pow10_exact(int k) {
     double p = 1.0;
@@ -239,6 +251,7 @@ RL_HD inline double round_to_double(uint64_t q, int b, bool sticky) {
 
 // correctly rounded D * 10^j (D < 2^48, any j in [-400, 400]) as strtod would
 RL_COLD double dec_to_double_big(int64_t D, int j) {
+    RL_COUNT_SLOW();
     Big X;
     bn_set_u64(X, (uint64_t)D);
     if (j >= 0) {
@@ -292,6 +305,7 @@ struct Dec14 {
 // round-trip through scratch, and scratch loads share vmcnt with the caller's
 // pending stores (every join after the call would wait for them)
 RL_COLD Dec14 dec14_slow_v(double a) {
+    RL_COUNT_SLOW();
     int64_t D;
     int E;
     uint64_t bits = dbits(a);

@@ -9,6 +9,7 @@
 // request's latency = completion time - its scheduled arrival time (so a late
 // generator does not hide queueing: no coordinated omission).  Prints one
 // JSON line with p50/p90/p99/p99.9 per QPS level.
+#include <dirent.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -27,7 +28,31 @@
 #include "../../include/rl_engine.h"
 #include "coalescer.hpp"
 
+extern "C" int rl_engine_debug_q14_slow(rl_engine* e, uint64_t* out);   // diagnostic (rl_engine.hip)
+
 namespace {
+
+// runqueue wait (ns) of every thread of this process: /proc/self/task/*/schedstat
+// field 2 (time spent runnable but not running)
+std::vector<std::pair<long, uint64_t>> run_delays() {
+    std::vector<std::pair<long, uint64_t>> out;
+    DIR* d = opendir("/proc/self/task");
+    if (!d) return out;
+    while (dirent* e = readdir(d)) {
+        if (e->d_name[0] == '.') continue;
+        char path[128];
+        snprintf(path, sizeof path, "/proc/self/task/%s/schedstat", e->d_name);
+        FILE* f = fopen(path, "r");
+        if (!f) continue;
+        unsigned long long run = 0, wait = 0;
+        if (fscanf(f, "%llu %llu", &run, &wait) == 2) out.push_back({atol(e->d_name), (uint64_t)wait});
+        fclose(f);
+    }
+    closedir(d);
+    return out;
+}
+
+size_t nb_cap(const std::string& slow) { return 4096 + slow.size(); }
 
 constexpr int64_t NS = 1000000000LL;
 constexpr int64_t T0_UNIX = 1760000000LL * NS;   // trace clock origin (as traces.py)
@@ -157,6 +182,7 @@ int main(int argc, char** argv) {
         std::vector<std::vector<int64_t>> bmax(G, std::vector<int64_t>(NBK, 0));
         std::vector<uint64_t> sent(G, 0), dropped(G, 0);
         std::atomic<int64_t> last_done{0};
+        const auto rd0 = run_delays();
         const int64_t start = rlc::steady_ns() + 20000000;   // 20 ms to spin up
         const int64_t stop = start + (int64_t)(a.seconds * NS);
         std::vector<std::thread> th;
@@ -228,6 +254,16 @@ int main(int argc, char** argv) {
         }
         for (auto& t : th) t.join();
         trace_clock += (int64_t)(a.seconds * NS) + NS;
+        // host scheduling: the largest runqueue wait any thread that lived
+        // through the level accumulated during it (the coalescer's submitter
+        // and completer among them)
+        uint64_t max_rq = 0, sum_rq = 0;
+        for (const auto& x : run_delays())
+            for (const auto& y : rd0)
+                if (x.first == y.first && x.second >= y.second) {
+                    max_rq = std::max<uint64_t>(max_rq, x.second - y.second);
+                    sum_rq += x.second - y.second;
+                }
         Hist h;
         uint64_t tot = 0, drop = 0;
         for (int g = 0; g < G; g++) { h.merge(hist[g]); tot += sent[g]; drop += dropped[g]; }
@@ -241,14 +277,76 @@ int main(int argc, char** argv) {
             for (int g = 0; g < G; g++) mx = std::max(mx, bmax[g][b]);
             tl += (b ? ", " : "") + std::to_string(mx / 1000);
         }
-        char buf[4096];
-        snprintf(buf, sizeof buf,
+        // stall attribution (RL_COALESCER_TRACE=<ring>): the batch whose oldest
+        // request waited longest, split into queue (waiting for a launch slot),
+        // stage-in (gather + H2D), enqueue (engine call), own device time (after
+        // the previous batch's results were back) and in-order wait behind it
+        std::string attr;
+        {
+            const std::vector<rlc::BatchTrace> tr = rlc::unwrap(c)->Trace();
+            int64_t worst = -1;
+            size_t wi = 0;
+            double mx[5] = {0, 0, 0, 0, 0};
+            std::string slow;   // [ms since start, stage-in us, enqueue us, own device us, m] of slow batches
+            uint64_t traced = 0;
+            for (size_t i = 1; i < tr.size(); i++) {
+                const rlc::BatchTrace& t = tr[i];
+                if (t.t_form < start) continue;
+                traced++;
+                const int64_t prev_done = tr[i - 1].t_done;
+                const double q = (t.t_form - t.t_submit) / 1e3, si = (t.t_h2d - t.t_form) / 1e3,
+                             en = (t.t_launched - t.t_h2d) / 1e3,
+                             behind = (std::max(prev_done, t.t_launched) - t.t_launched) / 1e3,
+                             own = (t.t_done - std::max(prev_done, t.t_launched)) / 1e3;
+                const double v[5] = {q, si, en, behind, own};
+                for (int k = 0; k < 5; k++) mx[k] = std::max(mx[k], v[k]);
+                if (t.t_done - t.t_submit > worst) { worst = t.t_done - t.t_submit; wi = i; }
+                if ((si > 1000 || en > 1000 || own > 1000) && slow.size() < 2000) {
+                    char x[160];
+                    snprintf(x, sizeof x, "%s[%.1f, %.0f, %.0f, %.0f, %llu]", slow.empty() ? "" : ", ",
+                             (t.t_form - start) / 1e6, si, en, own, (unsigned long long)t.m);
+                    slow += x;
+                }
+            }
+            if (traced) {
+                std::vector<char> abv(64 + nb_cap(slow));
+                char* ab = abv.data();
+                std::string nb;
+                for (size_t i = wi >= 4 ? wi - 4 : 1; i <= wi + 1 && i < tr.size(); i++) {
+                    const rlc::BatchTrace& t = tr[i];
+                    const int64_t pd = tr[i - 1].t_done;
+                    char x[256];
+                    snprintf(x, sizeof x, "%s{\"m\": %llu, \"queue_us\": %.1f, \"stage_in_us\": %.1f, \"enqueue_us\": %.1f, "
+                             "\"behind_prev_us\": %.1f, \"own_device_us\": %.1f}", nb.empty() ? "" : ", ",
+                             (unsigned long long)t.m, (t.t_form - t.t_submit) / 1e3, (t.t_h2d - t.t_form) / 1e3,
+                             (t.t_launched - t.t_h2d) / 1e3, (std::max(pd, t.t_launched) - t.t_launched) / 1e3,
+                             (t.t_done - std::max(pd, t.t_launched)) / 1e3);
+                    nb += x;
+                }
+                snprintf(ab, abv.size(),
+                         ", \"trace\": {\"batches\": %llu, \"max_queue_us\": %.1f, \"max_stage_in_us\": %.1f, "
+                         "\"max_enqueue_us\": %.1f, \"max_behind_prev_us\": %.1f, \"max_own_device_us\": %.1f, "
+                         "\"worst_wait_us\": %.1f, \"worst_and_neighbours\": [%s], "
+                         "\"slow_batches [ms, stage_in_us, enqueue_us, own_device_us, m]\": [%s]}",
+                         (unsigned long long)traced, mx[0], mx[1], mx[2], mx[3], mx[4], worst / 1e3, nb.c_str(),
+                         slow.c_str());
+                attr = ab;
+            }
+        }
+        std::vector<char> bufv(8192 + attr.size());
+        char* buf = bufv.data();
+        uint64_t slow_q14 = 0;
+        (void)rl_engine_debug_q14_slow(e, &slow_q14);
+        attr += ", \"q14_slow_calls_so_far\": " + std::to_string(slow_q14);
+        attr += ", \"max_thread_runqueue_wait_us\": " + std::to_string(max_rq / 1000) +
+                ", \"sum_thread_runqueue_wait_us\": " + std::to_string(sum_rq / 1000);
+        snprintf(buf, bufv.size(),
                  "%s{\"offered_qps\": %.0f, \"achieved_decisions_per_s\": %.1f, \"requests\": %llu, \"dropped\": %llu, "
                  "\"p50_us\": %.1f, \"p90_us\": %.1f, \"p99_us\": %.1f, \"p999_us\": %.1f, \"batches\": %llu, "
-                 "\"mean_batch\": %.1f, \"max_us_by_100ms\": [%s]}",
+                 "\"mean_batch\": %.1f, \"max_us_by_100ms\": [%s]%s}",
                  levels.empty() ? "" : ", ", qps, tot / span, (unsigned long long)tot, (unsigned long long)drop,
                  h.pct(50), h.pct(90), h.pct(99), h.pct(99.9), (unsigned long long)nb,
-                 nb ? (double)(s1.decided - s0.decided) / nb : 0.0, tl.c_str());
+                 nb ? (double)(s1.decided - s0.decided) / nb : 0.0, tl.c_str(), attr.c_str());
         levels += buf;
         fprintf(stderr, "level %.0f qps done: %s\n", qps, buf);
     }

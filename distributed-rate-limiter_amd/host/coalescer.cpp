@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 #include <chrono>
 
@@ -16,16 +18,43 @@ int64_t steady_ns() {
 }
 
 // per request: key 8 + ts 8 + n 8 + rem 8 + retry 8 + reset 8 + cfg 4 + dec 1
-Sub::Sub(size_t m_) : m(m_), left(m_), mem(new uint8_t[m_ * 53 + 8]) {
+Sub::Sub(size_t m_) : mem(new uint8_t[(m_ ? m_ : 1) * 53 + 8]), cap(m_ ? m_ : 1) { carve(m_); }
+
+void Sub::carve(size_t m_) {
+    first = 0;
+    m = m_;
+    taken = 0;
+    left = m_;
+    status = RL_OK;
+    reset_op = done = waiting = false;
+    done_ns = submit_ns = 0;
+    // layout by capacity, so a reused buffer keeps its arrays in place
+    const size_t c = cap;
     uint8_t* p = mem.get();
     key = reinterpret_cast<uint64_t*>(p);
-    ts = reinterpret_cast<int64_t*>(p + 8 * m);
-    n = reinterpret_cast<int64_t*>(p + 16 * m);
-    rem = reinterpret_cast<int64_t*>(p + 24 * m);
-    retry = reinterpret_cast<int64_t*>(p + 32 * m);
-    reset = reinterpret_cast<int64_t*>(p + 40 * m);
-    cfg = reinterpret_cast<uint32_t*>(p + 48 * m);
-    dec = p + 52 * m;
+    ts = reinterpret_cast<int64_t*>(p + 8 * c);
+    n = reinterpret_cast<int64_t*>(p + 16 * c);
+    rem = reinterpret_cast<int64_t*>(p + 24 * c);
+    retry = reinterpret_cast<int64_t*>(p + 32 * c);
+    reset = reinterpret_cast<int64_t*>(p + 40 * c);
+    cfg = reinterpret_cast<uint32_t*>(p + 48 * c);
+    dec = p + 52 * c;
+}
+
+// Completion waits: the runtime's (default), or polling the event
+// (RL_COALESCER_POLL=1, one busy core per waiting thread).  The A/B in
+// DESIGN.md (configs[4] tail) found the same rare stalls either way.
+static bool poll_waits() {
+    static const bool p = getenv("RL_COALESCER_POLL") != nullptr;
+    return p;
+}
+static hipError_t await_event(hipEvent_t ev) {
+    if (!poll_waits()) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t r = hipEventQuery(ev);
+        if (r != hipErrorNotReady) return r;
+        for (int i = 0; i < 32; i++) __builtin_ia32_pause();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -42,6 +71,7 @@ public:
         for (auto& d : dev_) {
             (void)hipFree(d.key);
             if (d.ev) (void)hipEventDestroy(d.ev);
+            if (d.ev_in) (void)hipEventDestroy(d.ev_in);
         }
         for (void* h : host_) (void)hipHostFree(h);
         if (cs_) (void)hipStreamDestroy(cs_);
@@ -64,6 +94,7 @@ public:
             if (hipMalloc(&dp, M * 61 + 64) != hipSuccess) return RL_ENOMEM;
             d.key = dp;
             if (hipEventCreateWithFlags(&d.ev, hipEventDisableTiming) != hipSuccess) return RL_EDEVICE;
+            if (hipEventCreateWithFlags(&d.ev_in, hipEventDisableTiming) != hipSuccess) return RL_EDEVICE;
         }
         M_ = M;
         return RL_OK;
@@ -78,8 +109,10 @@ public:
         ok &= hipMemcpyAsync(dv.ts, s.ts, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
         ok &= hipMemcpyAsync(dv.n, s.n, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
         ok &= hipMemcpyAsync(dv.cfg, s.cfg, 4 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
-        ok &= hipStreamSynchronize(cs_) == hipSuccess;
+        ok &= hipEventRecord(d.ev_in, cs_) == hipSuccess;
+        ok &= await_event(d.ev_in) == hipSuccess;
         if (!ok) return RL_EDEVICE;
+        s.t_h2d = steady_ns();
         int rc = rl_decide_batch_device(e_, m, dv.key, dv.ts, dv.n, dv.cfg, nullptr, dv.dec, dv.rem, dv.retry,
                                         dv.reset, nullptr, os_);
         if (rc != RL_OK) return rc;
@@ -92,7 +125,7 @@ public:
     }
     int wait(int i, Slot&) override {
         (void)hipSetDevice(dev_id_);   // the completer thread
-        return hipEventSynchronize(dev_[i].ev) == hipSuccess ? RL_OK : RL_EDEVICE;
+        return await_event(dev_[i].ev) == hipSuccess ? RL_OK : RL_EDEVICE;
     }
     int reset(uint32_t cfg, uint64_t key, int64_t ts) override {
         (void)hipSetDevice(dev_id_);   // the submitter thread
@@ -102,7 +135,8 @@ public:
 private:
     struct Dev {
         uint8_t* key = nullptr;   // base of the slot's device block
-        hipEvent_t ev = nullptr;
+        hipEvent_t ev = nullptr;       // results back on the host
+        hipEvent_t ev_in = nullptr;    // inputs on the device
     };
     // SoA layout of one slot block: key ts n | cfg | rem retry reset | dec
     static void carve(uint8_t* p, size_t M, Slot& s) {
@@ -147,6 +181,7 @@ public:
         return RL_OK;
     }
     int launch(int, Slot& s) override {
+        s.t_h2d = steady_ns();
         return fn_(user_, s.m, s.key, s.ts, s.n, s.cfg, s.dec, s.rem, s.retry, s.reset);
     }
     int wait(int, Slot&) override { return RL_OK; }
@@ -174,6 +209,7 @@ Coalescer::Coalescer(std::unique_ptr<Backend> be, const rl_coalescer_opts& o) : 
     if (o_.max_in_flight > 3) o_.max_in_flight = 3;
     if (o_.queue_cap == 0) o_.queue_cap = 1ull << 24;
     if (o_.linger_ns < 0) o_.linger_ns = 0;
+    if (const char* v = getenv("RL_COALESCER_TRACE")) trace_cap_ = (size_t)strtoull(v, nullptr, 10);
 }
 
 int Coalescer::start() {
@@ -187,6 +223,7 @@ int Coalescer::start() {
 Coalescer::~Coalescer() {
     Shutdown();
     for (auto& kv : subs_) delete kv.second;
+    for (Sub* s : pool_) delete s;
 }
 
 void Coalescer::Shutdown() {
@@ -214,21 +251,19 @@ void Coalescer::Shutdown() {
 int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
                       uint64_t* ticket, bool reset_op) {
     if (!ticket || (m && (!key || !ts || !n || !cfg)) || (reset_op && m != 1)) return RL_EINVAL;
-    Sub* s = new Sub(m);
+    Sub* s = get_sub(m);
     s->reset_op = reset_op;
+    if (trace_cap_) s->submit_ns = steady_ns();
     memcpy(s->key, key, 8 * m);
     memcpy(s->ts, ts, 8 * m);
     memcpy(s->n, n, 8 * m);
     memcpy(s->cfg, cfg, 4 * m);
     {
         std::lock_guard<std::mutex> g(mu_);
-        if (stop_) {
-            delete s;
-            return RL_ECLOSED;
-        }
-        if (pending_ + m > o_.queue_cap) {
-            delete s;
-            return RL_EAGAIN;
+        if (stop_ || pending_ + m > o_.queue_cap) {
+            const int rc = stop_ ? RL_ECLOSED : RL_EAGAIN;
+            put_sub(s);
+            return rc;
         }
         s->first = next_seq_;
         // an empty submission is done at once; its ticket must still be unique
@@ -275,8 +310,45 @@ int Coalescer::Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* 
     if (reset) memcpy(reset, s->reset, 8 * m);
     if (done_ns) *done_ns = s->done_ns;
     int st = s->status;
-    delete s;
+    put_sub(s);
     return st;
+}
+
+Sub* Coalescer::get_sub(size_t m) {
+    {
+        std::lock_guard<std::mutex> g(pool_mu_);
+        for (size_t i = pool_.size(); i-- > 0;) {
+            Sub* s = pool_[i];
+            if (s->cap >= m && s->cap <= 4 * m + 4096) {   // fits, and not far too big
+                pool_[i] = pool_.back();
+                pool_.pop_back();
+                s->carve(m);
+                return s;
+            }
+        }
+    }
+    return new Sub(m);
+}
+
+void Coalescer::put_sub(Sub* s) {
+    {
+        std::lock_guard<std::mutex> g(pool_mu_);
+        if (pool_.size() < 256 && s->cap <= (1u << 20)) {
+            pool_.push_back(s);
+            return;
+        }
+    }
+    delete s;
+}
+
+std::vector<BatchTrace> Coalescer::Trace() {
+    std::lock_guard<std::mutex> g(mu_);
+    std::vector<BatchTrace> out;
+    if (trace_.size() < trace_cap_) return trace_;
+    const size_t h = done_batches_ % trace_cap_;
+    out.insert(out.end(), trace_.begin() + h, trace_.end());
+    out.insert(out.end(), trace_.begin(), trace_.begin() + h);
+    return out;
 }
 
 rl_coalescer_stats Coalescer::Stats() {
@@ -333,6 +405,7 @@ void Coalescer::submitter() {
         pending_ -= m;
         inflight_++;
         lk.unlock();
+        if (trace_cap_) s.t_form = steady_ns();
         // the submissions' inputs are immutable after Submit: copy unlocked
         for (const auto& p : s.parts) {
             memcpy(s.key + p.at, p.sub->key + p.off, 8 * p.count);
@@ -342,6 +415,7 @@ void Coalescer::submitter() {
         }
         s.m = m;
         s.status = be_->launch(si, s);
+        if (trace_cap_) s.t_launched = steady_ns();
         lk.lock();
         st_.batches++;
         st_.max_batch_seen = std::max<uint64_t>(st_.max_batch_seen, m);
@@ -364,6 +438,7 @@ void Coalescer::completer() {
             si = launched_.front();
         }
         Slot& s = slots_[si];
+        const int64_t t_wait = trace_cap_ ? steady_ns() : 0;
         int st = s.status == RL_OK ? be_->wait(si, s) : s.status;
         for (const auto& p : s.parts) {
             memcpy(p.sub->dec + p.off, s.dec + p.at, p.count);
@@ -378,6 +453,13 @@ void Coalescer::completer() {
             wake = sub_idle_;
             launched_.pop_front();
             inflight_--;
+            if (trace_cap_) {
+                BatchTrace t{done_batches_, s.m, 0, s.t_form, s.t_h2d, s.t_launched, t_wait, now};
+                t.t_submit = s.parts.empty() ? s.t_form : s.parts[0].sub->submit_ns;   // the oldest request
+                if (trace_.size() < trace_cap_) trace_.push_back(t);
+                else trace_[done_batches_ % trace_cap_] = t;
+            }
+            done_batches_++;
             st_.decided += s.m;
             for (const auto& p : s.parts) {
                 Sub* sub = p.sub;

@@ -35,6 +35,7 @@ struct Slot {
     int64_t* reset = nullptr;
     size_t m = 0;
     int status = RL_OK;
+    int64_t t_form = 0, t_h2d = 0, t_launched = 0;   // steady ns (batch trace)
     struct Part {
         struct Sub* sub;
         size_t off, count, at;   // sub[off, off+count) <-> slot[at, at+count)
@@ -66,16 +67,29 @@ struct Sub {
     bool done = false;
     bool waiting = false;         // a caller blocks on cv (else completion skips the wake)
     int64_t done_ns = 0;          // steady clock at completion
+    int64_t submit_ns = 0;        // steady clock at Submit (batch trace)
     std::condition_variable cv;
     std::unique_ptr<uint8_t[]> mem;
     uint64_t* key;
     int64_t *ts, *n, *rem, *retry, *reset;
     uint32_t* cfg;
     uint8_t* dec;
+    size_t cap = 0;               // requests the buffer holds (pooled Subs are reused)
     explicit Sub(size_t m);
+    void carve(size_t m);         // reset for a new submission of m <= cap requests
 };
 
 int64_t steady_ns();
+
+// One launched batch, for stall attribution (RL_COALESCER_TRACE=<ring size>):
+// steady-clock ns of the oldest request's Submit, the batch taken from the
+// queue, inputs on the device (H2D done), the engine call returned, the
+// completer starting to wait, and the results back on the host.
+struct BatchTrace {
+    uint64_t seq;
+    uint64_t m;
+    int64_t t_submit, t_form, t_h2d, t_launched, t_wait, t_done;
+};
 
 class Coalescer {
 public:
@@ -89,10 +103,18 @@ public:
              int64_t* done_ns = nullptr);
     rl_coalescer_stats Stats();
     void Shutdown();
+    // the trace ring, oldest first (empty unless RL_COALESCER_TRACE is set)
+    std::vector<BatchTrace> Trace();
 
 private:
     void submitter();
     void completer();
+    // pooled submissions: no heap allocation (and no mmap / page faults for
+    // large ones) per Submit in steady state
+    Sub* get_sub(size_t m);
+    void put_sub(Sub* s);
+    std::mutex pool_mu_;
+    std::vector<Sub*> pool_;
 
     std::unique_ptr<Backend> be_;
     rl_coalescer_opts o_;
@@ -107,6 +129,9 @@ private:
     bool stop_ = false, sub_exited_ = false;
     bool sub_idle_ = false;        // the submitter sleeps on cv_sub_ (submit wakes it only then)
     rl_coalescer_stats st_{};
+    std::vector<BatchTrace> trace_;   // ring of trace_cap_ batches
+    size_t trace_cap_ = 0;
+    uint64_t done_batches_ = 0;
     std::thread t_sub_, t_done_;
 };
 
