@@ -16,6 +16,11 @@
 //     one exact division residual gives the 14-digit integer D and its rounding
 //     direction; D / 10^k (or D * 10^k) is then a single correctly rounded IEEE
 //     operation because D < 2^47 and 10^k (k <= 22) are exact doubles;
+//   * wide path, 1e-345 < |x| < 1e-9 (normal doubles): 128-bit truncated
+//     powers of five (rl_pow5.h) give D, and D * 10^j back to a double, with
+//     a proven error bound; a result the bound cannot decide (never seen in
+//     fuzzing: it needs a remainder within 2^-70 of a rounding midpoint) falls
+//     through to
 //   * slow path, everything else: fixed-width big-integer arithmetic.
 // All code here must be compiled with -ffp-contract=off.
 #pragma once
@@ -72,8 +77,9 @@ RL_INLINE double bitsd(uint64_t u) {
 RL_INLINE int floor_log10_pow2(int e2) { return (e2 * 78913) >> 18; }
 
 // Round a * 10^k (a > 0, |k| <= 22, result < 2^47) to the nearest integer,
-// ties to even, exactly.
-RL_INLINE int64_t round_scaled(double a, int k) {
+// ties to even, exactly; ge: the exact a * 10^k >= lo (an integer-valued
+// double), which the rounded result cannot tell when it rounds up onto lo.
+RL_INLINE int64_t round_scaled_ge(double a, int k, double lo, bool& ge) {
     double p, err;
     if (k >= 0) {
         double P = pow10_exact(k);
@@ -84,6 +90,7 @@ RL_INLINE int64_t round_scaled(double a, int k) {
         p = a / P;
         err = __builtin_fma(-p, P, a);          // a - p*P, exact; sign = direction
     }
+    ge = (p > lo) || (p == lo && err >= 0.0);
     double d0 = floor(p);
     double f = p - d0;                           // exact (p has few fraction bits)
     int64_t D = (int64_t)d0;
@@ -92,6 +99,10 @@ RL_INLINE int64_t round_scaled(double a, int k) {
     else if (f < 0.5) up = false;
     else up = (err > 0.0) || (err == 0.0 && (D & 1));
     return D + (up ? 1 : 0);
+}
+RL_INLINE int64_t round_scaled(double a, int k) {
+    bool ge;
+    return round_scaled_ge(a, k, 0.0, ge);
 }
 
 // Correctly rounded d / P for an integer-valued d in [1, 2^53) and P = 10^k,
@@ -114,6 +125,77 @@ RL_INLINE double div_pow10(double d, double P, double R) {
 }
 
 // RNE(x * P) exactly, for x > 0, P = 10^k exact (k <= 22), x*P < 2^47
+#include "rl_pow5.h"
+
+// ---------------------------------------------------------------------------
+// wide path (cold): 192-bit products with 128-bit powers of five
+// ---------------------------------------------------------------------------
+typedef unsigned __int128 u128;
+
+// (w2:w1:w0) = m * (fhi:flo)
+RL_INLINE void mul_64x128(uint64_t m, uint64_t fhi, uint64_t flo, uint64_t& w2, uint64_t& w1, uint64_t& w0) {
+    const u128 a = (u128)m * flo, b = (u128)m * fhi;
+    w0 = (uint64_t)a;
+    const u128 mid = (a >> 64) + (u128)(uint64_t)b;
+    w1 = (uint64_t)mid;
+    w2 = (uint64_t)(b >> 64) + (uint64_t)(mid >> 64);
+}
+
+// RNE(W' * 2^-t) where the exact W' lies in [W, W + err), W = (w2:w1:w0),
+// 64 <= t <= 191, err < 2^64: q = floor(W * 2^-t) (must fit 64 bits) and
+// whether to round up.  False when [W, W + err) straddles the midpoint.
+RL_INLINE bool round_shift192(uint64_t w2, uint64_t w1, uint64_t w0, int t, uint64_t err, uint64_t& q, bool& up) {
+    if (t < 64 || t > 191) return false;
+    const int s = t - 64;
+    const u128 hi = ((u128)w2 << 64) | w1;
+    const u128 qq = hi >> s;
+    if ((uint64_t)(qq >> 64)) return false;
+    q = (uint64_t)qq;
+    // remainder R = (rh : w0), rh < 2^s; the midpoint 2^(t-1)
+    const u128 rh = s ? (hi & (((u128)1 << s) - 1)) : 0;
+    const u128 hh = s ? ((u128)1 << (s - 1)) : 0;
+    const uint64_t hl = s ? 0 : (1ull << 63);
+    const bool gt_half = rh > hh || (rh == hh && w0 > hl);          // R > half
+    const uint64_t e0 = w0 + err;
+    const u128 eh = rh + (e0 < w0 ? 1 : 0);                          // R + err = (eh : e0)
+    const bool le_half = eh < hh || (eh == hh && e0 <= hl);          // R + err <= half
+    if (gt_half) { up = true; return true; }
+    if (le_half) { up = false; return true; }
+    return false;
+}
+
+// RNE(m * 2^e * 10^k), k in [POW5_KMIN, POW5_KMAX], result < 2^62, and
+// floor(m * 2^e * 10^k) in Dfloor
+RL_INLINE bool round_scaled_wide(uint64_t m, int e, int k, int64_t& D, int64_t& Dfloor) {
+    const Pow5 p = pow5_pos(k);                 // 5^k = (F + theta) 2^sh
+    uint64_t w2, w1, w0, q;
+    mul_64x128(m, p.hi, p.lo, w2, w1, w0);      // exact product in [W, W + m)
+    bool up;
+    if (!round_shift192(w2, w1, w0, -(p.sh + e + k), m, q, up)) return false;
+    if (q >= (1ull << 62)) return false;
+    D = (int64_t)(q + (up ? 1 : 0));
+    Dfloor = (int64_t)q;
+    return true;
+}
+
+// correctly rounded D * 10^-n (strtod), n in [POW5_KMIN, POW5_KMAX], 0 < D < 2^63;
+// false when undecided or the result is not a normal double
+RL_INLINE bool dec_value_wide(uint64_t D, int n, double& out) {
+    const Pow5 p = pow5_neg(n);                 // 5^-n = (G + theta) 2^-sh
+    uint64_t w2, w1, w0, q;
+    mul_64x128(D, p.hi, p.lo, w2, w1, w0);      // exact product in [W, W + D)
+    const int L = w2 ? 128 + 64 - __builtin_clzll(w2) : (w1 ? 64 + 64 - __builtin_clzll(w1) : 64 - __builtin_clzll(w0));
+    int t = L - 53;
+    bool up;
+    if (!round_shift192(w2, w1, w0, t, D, q, up)) return false;
+    q += up ? 1 : 0;
+    if (q == (1ull << 53)) { q >>= 1; t++; }
+    const int ex = t - p.sh - n;                // value = q * 2^ex, q in [2^52, 2^53)
+    if (ex + 52 < -1022 || ex + 52 > 1023) return false;
+    out = ldexp((double)q, ex);
+    return true;
+}
+
 RL_INLINE int64_t round_scaled_P(double x, double P) {
     double p = x * P;
     double err = __builtin_fma(x, P, -p);
@@ -213,7 +295,7 @@ RL_HD inline uint64_t bn_divmod_small_q(Big& N, const Big& Q, int qbits) {
 }
 
 // exact round(a * 10^k) to nearest-even integer (result < 2^48); a = m * 2^e
-RL_COLD int64_t round_scaled_big(uint64_t m, int e, int k) {
+RL_COLD int64_t round_scaled_big(uint64_t m, int e, int k, int64_t* floor_out = nullptr) {
     Big N, Q;
     bn_set_u64(N, m);
     bn_set_u64(Q, 1);
@@ -222,6 +304,7 @@ RL_COLD int64_t round_scaled_big(uint64_t m, int e, int k) {
     else { bn_mul_pow5(Q, -k); s = e + k; }
     if (s >= 0) bn_shl(N, s); else bn_shl(Q, -s);
     uint64_t D = bn_divmod_small_q(N, Q, 50);
+    if (floor_out) *floor_out = (int64_t)D;
     // compare 2*rem with Q
     bn_shl(N, 1);
     int c = bn_cmp(N, Q);
@@ -251,6 +334,10 @@ RL_HD inline double round_to_double(uint64_t q, int b, bool sticky) {
 
 // correctly rounded D * 10^j (D < 2^48, any j in [-400, 400]) as strtod would
 RL_COLD double dec_to_double_big(int64_t D, int j) {
+    if (j < 0 && -j >= POW5_KMIN && -j <= POW5_KMAX && D > 0) {
+        double v;
+        if (dec_value_wide((uint64_t)D, -j, v)) return v;
+    }
     RL_COUNT_SLOW();
     Big X;
     bn_set_u64(X, (uint64_t)D);
@@ -288,8 +375,11 @@ RL_INLINE bool dec14_fast(double a, int64_t& D, int& E) {
     int E0 = floor_log10_pow2(e2);
     if (E0 < -9 || E0 > 34) return false;
     const int64_t LO = 10000000000000LL, HI = 100000000000000LL;
-    int64_t D1 = round_scaled(a, 12 - E0);       // try E = E0 + 1
-    if (D1 >= LO) { D = D1; E = E0 + 1; return true; }
+    // a >= 10^(E0+1) exactly (a value just below it can ROUND onto 1e13 at
+    // E0+1 digits, and its 14 digits are still those of decade E0)
+    bool ge;
+    int64_t D1 = round_scaled_ge(a, 12 - E0, (double)LO, ge);   // try E = E0 + 1
+    if (ge) { D = D1; E = E0 + 1; return true; }
     int64_t D0 = round_scaled(a, 13 - E0);
     if (D0 >= HI) { D = LO; E = E0 + 1; }        // rounding carried into the next decade
     else { D = D0; E = E0; }
@@ -305,7 +395,6 @@ struct Dec14 {
 // round-trip through scratch, and scratch loads share vmcnt with the caller's
 // pending stores (every join after the call would wait for them)
 RL_COLD Dec14 dec14_slow_v(double a) {
-    RL_COUNT_SLOW();
     int64_t D;
     int E;
     uint64_t bits = dbits(a);
@@ -317,8 +406,20 @@ RL_COLD Dec14 dec14_slow_v(double a) {
     int e2 = e + L - 1;                           // a in [2^e2, 2^(e2+1))
     int E0 = floor_log10_pow2(e2);
     const int64_t LO = 10000000000000LL, HI = 100000000000000LL;
-    int64_t D1 = round_scaled_big(m, e, 12 - E0);
-    if (D1 >= LO) return Dec14{D1, E0 + 1};
+    if (ex != 0 && 12 - E0 >= POW5_KMIN && 13 - E0 <= POW5_KMAX) {
+        int64_t D1, D0, F1, F0;
+        if (round_scaled_wide(m, e, 12 - E0, D1, F1)) {
+            if (F1 >= LO) return Dec14{D1, E0 + 1};   // a >= 10^(E0+1): exact, not rounded onto LO
+            if (round_scaled_wide(m, e, 13 - E0, D0, F0)) {
+                if (D0 >= HI) return Dec14{LO, E0 + 1};
+                return Dec14{D0, E0};
+            }
+        }
+    }
+    RL_COUNT_SLOW();
+    int64_t F1 = 0;
+    int64_t D1 = round_scaled_big(m, e, 12 - E0, &F1);
+    if (F1 >= LO) return Dec14{D1, E0 + 1};
     int64_t D0 = round_scaled_big(m, e, 13 - E0);
     if (D0 >= HI) { D = LO; E = E0 + 1; } else { D = D0; E = E0; }
     return Dec14{D, E};

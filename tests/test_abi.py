@@ -44,6 +44,16 @@ def test_q14_host_instantiation(rl):
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
 
 
+def test_q14_host_decade_edges_and_tiny(rl):
+    # regression: a value just below 10^k must keep decade k-1's 14 digits
+    # (0.99999999999999 stays, it does not become 1)
+    from tracegen import q14_edge_values
+    x = q14_edge_values()
+    got = rl.q14_host(x)
+    ref = np.array([float("%.14g" % v) for v in x])
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64))
+
+
 def test_host_mirror_without_gpu(rl):
     # config_test.go:8-178: Validate messages
     S, M, H = 10 ** 9, 60 * 10 ** 9, 3600 * 10 ** 9

@@ -76,6 +76,15 @@ def test_q14_device_matches_glibc(rl):
     assert np.array_equal(host[::50].view(np.uint64), ref.view(np.uint64))
 
 
+def test_q14_device_decade_edges_and_tiny(rl):
+    from tracegen import q14_edge_values
+    eng = make_engine(rl, 0, tb=1024, win=1024, max_batch=1024)
+    x = q14_edge_values(seed=9)
+    dev = eng.q14_device(x)
+    ref = np.array([float("%.14g" % v) for v in x])
+    assert np.array_equal(dev.view(np.uint64), ref.view(np.uint64))
+
+
 # --- randomized multi-config traces, multiple batches (state carried) ----------
 
 @pytest.mark.parametrize("profile", [0, 1])

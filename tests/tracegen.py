@@ -51,3 +51,23 @@ def skewed_trace(seed, m, nkeys, configs, skews_ns=(0, -2_500_000_000, -7 * NS, 
     cfg = (keys % len(configs)).astype(np.uint32)
     sms = true_t // 1_000_000
     return keys, ts, n, cfg, sms
+
+
+def q14_edge_values(n=4000, seed=5):
+    """values just below / at / above powers of ten (where rounding to 14
+    digits carries into the next decade, or must not), 14-digit midpoints,
+    and log-uniform tiny magnitudes down to 1e-340 (the wide and big-integer
+    paths of rl_q14.h)"""
+    rng = np.random.default_rng(seed)
+    j = rng.integers(-330, 30, n)
+    u = 10.0 ** rng.uniform(-17, -12, n)
+    p10 = np.array([float(f"1e{k}") for k in j])
+    below = p10 * (1.0 - u)
+    above = p10 * (1.0 + u)
+    D = rng.integers(10 ** 13, 10 ** 14, n)
+    mids = np.array([float(f"{d}5e{k - 14}") for d, k in zip(D, j)])
+    tiny = 10.0 ** rng.uniform(-340, -9, n) * rng.choice([-1.0, 1.0], n)
+    fixed = [0.99999999999999, 0.999999999999994, 0.999999999999996, 9.9999999999999e-10, 999999999999.99,
+             9.99999999999994e-300, 2.2250738585072014e-308, 1e-9, 1e-10, 1e-300]
+    x = np.concatenate([below, above, mids, tiny, fixed])
+    return x[np.isfinite(x) & (x != 0)]
