@@ -452,7 +452,9 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         eng.decide_device(mm, key, ts, n, cfg, sms, dec, rem, retry, reset, None, stream)
 
     router = rl_amd.Router(local_rank, world, m, world * m)
-    pipe = shard.RoutedPipeline(router, decide, world, m, dev, pg_req=None, pg_res=pg_res)
+    pipe = shard.RoutedPipeline(router, decide, world, m, dev, pg_req=None, pg_res=pg_res,
+                                depth=int(os.environ.get("RL_ROUTE_DEPTH", "6")),
+                                lookahead=int(os.environ.get("RL_ROUTE_LOOKAHEAD", "2")))
     outs = [(torch.empty(m, dtype=torch.uint8, device=dev),) +
             tuple(torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)) for _ in range(pipe.depth)]
     recv = []
@@ -461,11 +463,12 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
         if rc != 0:
             raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}")
-    eng.set_timing(1)
+    eng.set_timing(0 if os.environ.get("RL_BENCH_NO_TIMING") else 1)
     eng.stage_times()
     dist.barrier()
     torch.cuda.synchronize()
     pipe.wait_s = 0.0
+    pipe.host_prof = {}
     t0 = time.perf_counter()
     pipe.run(ins[args.warmup:], [outs[b % pipe.depth] for b in range(args.steps)],
              done=lambda b, S: recv.append(pipe.last_recv))
@@ -495,11 +498,14 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         "batch": m,
         "received_per_step": {"mean_over_ranks": float(agg[:, 2].sum() / world / args.steps),
                               "max_rank_step": float(agg[:, 1].max())},
-        "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
+        "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3}
+        | {k: v / args.steps * 1e3 for k, v in pipe.host_prof.items()},
         "roofline": roof,
     }
     eng.close()
     router.close()
+    del pipe, outs, ins
+    rl_amd.release_dedicated_streams()
     return res
 
 
@@ -561,7 +567,14 @@ def main():
         # results on a second one (its own stream), barrier and timing
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
-        dist.init_process_group("nccl", device_id=dev)
+        # the request group's internal stream at high priority: a hardware
+        # queue apart from the result group's, whose stream waits on the
+        # engine (a waiting stream blocks the streams that share its queue)
+        opts = None
+        if not os.environ.get("RL_ROUTE_PG_NORMAL"):
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=dev, pg_options=opts)
         pg_res = dist.new_group(backend="nccl")
     if ingress == "routed":
         res = bench_routed(args, workload, world, rank, local_rank, dev, pg_res)

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "../../include/rl_route.h"
 #include "rl_sort.h"
@@ -28,7 +29,7 @@ using namespace rl;
 namespace {
 
 constexpr int RT_BLOCK = 256;
-constexpr int RT_ITEMS = 16;
+constexpr int RT_ITEMS = 4;                    // 1024-request tiles: ~1000 blocks per 1M batch
 constexpr int RT_TILE = RT_BLOCK * RT_ITEMS;   // requests per pack tile
 constexpr int MAX_WORLD = 64;
 constexpr int MERGE_PASSES = 4;                // 32-bit time keys, 8-bit digits
@@ -37,6 +38,20 @@ constexpr int MERGE_PASSES = 4;                // 32-bit time keys, 8-bit digits
 constexpr uint32_t RS_SPAN = 1u;               // received ts span >= 2^32 ns
 
 __device__ inline uint32_t owner_of(uint64_t k, uint32_t world) { return (uint32_t)(mix64(k) >> 32) % world; }
+
+// lanes of this wave holding the same owner id as this lane (ballots over the
+// id's bits; world <= 64, so at most 6), restricted to `valid`
+__device__ inline uint64_t owner_peers(uint32_t own, uint32_t world, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+        if ((1u << b) >= world) break;   // wave-uniform
+        const uint32_t bit = (own >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    return peers;
+}
 
 __global__ __launch_bounds__(RT_BLOCK) void k_route_owner(uint32_t m, const uint64_t* __restrict__ key,
                                                           uint32_t world, uint32_t* __restrict__ owner) {
@@ -65,18 +80,29 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint6
     if (threadIdx.x == 0) s_uns = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * RT_TILE;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long lo = ~0ull, hi = 0;
     uint32_t uns = 0;
 #pragma unroll
     for (int j = 0; j < RT_ITEMS; j++) {
+        // a wave's 64 requests are consecutive: the predecessor's ts is the
+        // lane below (lane 0 loads it)
         const uint32_t i = base + j * RT_BLOCK + threadIdx.x;
-        if (i < m) {
-            atomicAdd(&s_cnt[owner_of(key[i], world)], 1u);
-            const int64_t t = ts[i];
+        const bool ok = i < m;
+        const uint32_t own = ok ? owner_of(key[i], world) : 0u;
+        const int64_t t = ok ? ts[i] : 0;
+        int64_t tp = __shfl_up(t, 1);
+        if (lane == 0) tp = (ok && i > 0) ? ts[i - 1] : t;
+        // one LDS add per owner per wave (not per request: at small world
+        // every request of a tile would hit one counter)
+        const uint64_t peers = owner_peers(own, world, ok);
+        if (ok && (peers & lt) == 0) atomicAdd(&s_cnt[own], (uint32_t)__popcll(peers));
+        if (ok) {
             const unsigned long long b = bias(t);
             lo = b < lo ? b : lo;
             hi = b > hi ? b : hi;
-            if (i > 0 && ts[i - 1] > t) uns = 1;
+            if (i > 0 && tp > t) uns = 1;
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -162,13 +188,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(uint32_t m, const ui
         const uint32_t i = base + j * 64 + lane;
         const bool ok = i < m;
         own[j] = ok ? owner_of(key[i], world) : 0u;
-        uint64_t peers = __ballot(ok);
-#pragma unroll
-        for (int b = 0; b < 6; b++) {   // world <= 64: match the 6-bit owner id
-            const uint32_t bit = (own[j] >> b) & 1u;
-            const uint64_t bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
-        }
+        const uint64_t peers = owner_peers(own[j], world, ok);
         if (ok) {
             const uint32_t below = __popcll(peers & lt);
             const uint32_t cur = s_wcnt[wave][own[j]];
@@ -367,6 +387,26 @@ extern "C" int rl_router_sync(rl_router* r, void* stream) {
     if (s & EF_LOOKBACK) return RL_ETIMEOUT;
     if (s & (RS_SPAN << 8)) return RL_EINVAL;
     return RL_OK;
+}
+
+extern "C" int rl_stream_create_dedicated(int32_t device, void** out) {
+    if (!out) return RL_EINVAL;
+    *out = nullptr;
+    if (hipSetDevice(device) != hipSuccess) return RL_EDEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return RL_EDEVICE;
+    const int ncu = prop.multiProcessorCount;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; c++) mask[c / 32] |= 1u << (c % 32);
+    hipStream_t st = nullptr;
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return RL_EDEVICE;
+    *out = st;
+    return RL_OK;
+}
+
+extern "C" int rl_stream_destroy(void* stream) {
+    if (!stream) return RL_EINVAL;
+    return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? RL_OK : RL_EDEVICE;
 }
 
 extern "C" int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner, void* stream) {

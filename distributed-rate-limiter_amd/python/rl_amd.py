@@ -155,6 +155,8 @@ _sig = {
     "rl_router_destroy": (C.c_int, [vp]),
     "rl_router_sync": (C.c_int, [vp, vp]),
     "rl_route_owner": (C.c_int, [vp, C.c_size_t, vp, vp, vp]),
+    "rl_stream_create_dedicated": (C.c_int, [C.c_int32, C.POINTER(vp)]),
+    "rl_stream_destroy": (C.c_int, [vp]),
     "rl_route_pack": (C.c_int, [vp, C.c_size_t] + [vp] * 8),
     "rl_route_merge": (C.c_int, [vp, C.c_size_t] + [vp] * 9),
     "rl_route_results": (C.c_int, [C.c_size_t] + [vp] * 7),
@@ -315,6 +317,24 @@ class Engine:
         return out
 
 
+_DEDICATED_STREAMS = []   # rl_stream_create_dedicated handles (release_dedicated_streams)
+
+
+def release_dedicated_streams():
+    """destroy every Router.dedicated_stream: call once nothing uses them any
+    more (pipelines and their tensors dropped); synchronizes the device and
+    empties torch's allocator cache first, whose blocks may carry events on
+    those streams"""
+    import gc
+
+    import torch
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    while _DEDICATED_STREAMS:
+        lib.rl_stream_destroy(_DEDICATED_STREAMS.pop())
+
+
 class Router:
     """rl_router (include/rl_route.h): the routing kernels of one rank.  All
     arguments are device pointers (ints) and a hipStream_t; asynchronous."""
@@ -326,10 +346,22 @@ class Router:
             raise EngineError(rc, "rl_router_create failed")
         self.h = h
         self.world = world
+        self.device = device
 
     def _chk(self, rc, what):
         if rc != RL_OK:
             raise EngineError(rc, what)
+
+    def dedicated_stream(self):
+        """a torch stream on a hardware queue of its own
+        (rl_stream_create_dedicated)"""
+        import torch
+        h = vp()
+        self._chk(lib.rl_stream_create_dedicated(self.device, C.byref(h)), "rl_stream_create_dedicated")
+        # kept for the life of the process: torch's allocator and process
+        # groups may still hold events on them after the router is closed
+        _DEDICATED_STREAMS.append(h)
+        return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", self.device))
 
     def owner(self, m, key, owner, stream):
         self._chk(lib.rl_route_owner(self.h, m, key, owner, stream), "rl_route_owner")
@@ -360,6 +392,7 @@ class Router:
         if self.h:
             lib.rl_router_destroy(self.h)
             self.h = None
+
 
     def __del__(self):
         try:

@@ -19,9 +19,14 @@ order consistent with each rank's own order, under one monotone store clock.
 """
 from __future__ import annotations
 
+import os
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
+
+_PROF = os.environ.get("RL_ROUTE_PROFILE") is not None
 
 _M1 = np.uint64(0xbf58476d1ce4e5b9)
 _M2 = np.uint64(0x94d049bb133111eb)
@@ -88,7 +93,19 @@ class RoutedPipeline:
         mr = max_recv or world * max_batch
         self.max_batch, self.max_recv = mb, mr
         d = self.dev
-        self.R = torch.cuda.Stream(d) if self.cuda else None
+        # streams on hardware queues of their own (ops.dedicated_stream): R and
+        # the S streams wait on the engine's events, and a waiting stream would
+        # block every stream that shares its hardware queue
+        mk = getattr(ops, "dedicated_stream", None)
+        if os.environ.get("RL_ROUTE_SHARED_QUEUES"):
+            mk = None
+
+        def new_stream():
+            if not self.cuda:
+                return None
+            return mk() if mk is not None else torch.cuda.Stream(d)
+
+        self.R = new_stream()
         self.slots = []
         for _ in range(depth):
             s = dict(
@@ -111,12 +128,22 @@ class RoutedPipeline:
                 reset=torch.empty(mr, dtype=torch.int64, device=d),
                 res=torch.empty((mr, 4), dtype=torch.int64, device=d),
                 back=torch.empty((mb, 4), dtype=torch.int64, device=d),
-                S=torch.cuda.Stream(d) if self.cuda else None,
+                S=new_stream(),
                 ev_cnt=None, ev_merged=None, ev_done=None, m=0, busy=False,
             )
             self.slots.append(s)
         self.last_recv = 0
         self.wait_s = 0.0          # host time spent waiting for count copies
+        self.host_prof = {}
+
+    def _tick(self, name):
+        """RL_ROUTE_PROFILE: host seconds per call site (since the last tick)"""
+        if not _PROF:
+            return
+        now = time.perf_counter()
+        if name is not None and getattr(self, "_t_last", None) is not None:
+            self.host_prof[name] = self.host_prof.get(name, 0.0) + now - self._t_last
+        self._t_last = now
 
     @staticmethod
     def _p(t):
@@ -143,12 +170,15 @@ class RoutedPipeline:
         assert m <= self.max_batch
         s["m"], s["busy"] = m, True
         p = self._p
+        self._tick(None)
         with _ctx(self.R):
             if s["ev_done"] is not None:
                 self.R.wait_event(s["ev_done"])   # the set's previous batch has finished
             self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]),
                           self._sp(self.R))
+            self._tick("a_pack")
             self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_req)
+            self._tick("a_a2a_cnt")
             s["cnt_h"][0].copy_(s["scnt"], non_blocking=True)
             s["cnt_h"][1].copy_(s["rcnt"], non_blocking=True)
             if self.cuda:
@@ -161,37 +191,44 @@ class RoutedPipeline:
         returns the stream on which they are complete"""
         s = self.slots[b % self.depth]
         if s["ev_cnt"] is not None:
-            import time
             t0 = time.perf_counter()
             s["ev_cnt"].synchronize()
             self.wait_s += time.perf_counter() - t0
+        self._tick("b_wait")
         sc = s["cnt_h"][0][:, 0].tolist()
         rc = s["cnt_h"][1][:, 0].tolist()
+        self._tick("b_counts")
         tot, m = int(sum(rc)), s["m"]
         assert tot <= self.max_recv, "received more than max_recv"
         self.last_recv = tot
         p = self._p
         with _ctx(self.R):
             self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
+            self._tick("b_a2a_req")
             self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]),
                            p(s["sms"]), p(s["at"]), self._sp(self.R))
             if self.cuda:
                 s["ev_merged"] = torch.cuda.Event()
                 s["ev_merged"].record(self.R)
+            self._tick("b_merge")
         S = s["S"]
         with _ctx(S):
             if S is not None:
                 S.wait_event(s["ev_merged"])
             self.decide(tot, p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]), p(s["sms"]), p(s["dec"]),
                         p(s["rem"]), p(s["retry"]), p(s["reset"]), self._sp(S))
+            self._tick("b_decide")
             self.ops.results(tot, p(s["at"]), p(s["dec"]), p(s["rem"]), p(s["retry"]), p(s["reset"]), p(s["res"]),
                              self._sp(S))
+            self._tick("b_results")
             self._a2a(s["back"][:m], s["res"][:tot], sc, rc, self.pg_res)
+            self._tick("b_a2a_res")
             self.ops.unpack(m, p(s["slot"]), p(s["back"]), p(dec), p(rem), p(retry), p(reset), self._sp(S))
             if S is not None:
                 s["ev_done"] = torch.cuda.Event()
                 s["ev_done"].record(S)
         s["busy"] = False
+        self._tick("b_unpack")
         return S
 
     def run(self, batches, outs, done=None):

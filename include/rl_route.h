@@ -76,6 +76,14 @@ int rl_router_destroy(rl_router* r);
  * sticky status (RL_EINVAL: ts span >= 2^32 ns, RL_ETIMEOUT: sort look-back) */
 int rl_router_sync(rl_router* r, void* stream);
 
+/* A stream on a hardware queue of its own (CU-masked with every CU, which
+ * the runtime never shares): with more streams than the process's hardware
+ * queues, a stream that waits on an event blocks every stream sharing its
+ * queue; the routed pipeline's streams wait on the engine's, so they need
+ * their own.  Returns a hipStream_t in *out. */
+int rl_stream_create_dedicated(int32_t device, void** out);
+int rl_stream_destroy(void* stream);
+
 /* owner of each key id (the partition: (mix64(k) >> 32) mod world) */
 int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner, void* stream);
 
