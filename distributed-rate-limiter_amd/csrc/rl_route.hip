@@ -68,14 +68,15 @@ struct PackSum {
     uint32_t unsorted;
 };
 
-__global__ void k_pack_init(PackSum* sum) { *sum = PackSum{~0ull, 0ull, 0u}; }
 
-// per-tile owner counts: tile_cnt[tile * world + o]; the batch summary
+// per-tile owner counts: tile_cnt[tile * world + o]; the tile's summary in
+// tile_sum[tile] (no global atomics: k_route_scan reduces the tiles)
 __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint64_t* __restrict__ key,
                                                          const int64_t* __restrict__ ts, uint32_t world,
-                                                         uint32_t* __restrict__ tile_cnt, PackSum* sum) {
+                                                         uint32_t* __restrict__ tile_cnt, PackSum* tile_sum) {
     __shared__ uint32_t s_cnt[MAX_WORLD];
     __shared__ uint32_t s_uns;
+    __shared__ unsigned long long s_lo[RT_BLOCK / 64], s_hi[RT_BLOCK / 64];
     if (threadIdx.x < MAX_WORLD) s_cnt[threadIdx.x] = 0;
     if (threadIdx.x == 0) s_uns = 0;
     __syncthreads();
@@ -111,12 +112,19 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint6
         hi = h2 > hi ? h2 : hi;
     }
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&sum->lo, lo);
-        atomicMax(&sum->hi, hi);
+        s_lo[threadIdx.x >> 6] = lo;
+        s_hi[threadIdx.x >> 6] = hi;
     }
     if (uns) s_uns = 1;
     __syncthreads();
-    if (threadIdx.x == 0 && s_uns) atomicOr(&sum->unsorted, 1u);
+    if (threadIdx.x == 0) {
+        PackSum t{~0ull, 0ull, s_uns};
+        for (int w = 0; w < RT_BLOCK / 64; w++) {
+            t.lo = s_lo[w] < t.lo ? s_lo[w] : t.lo;
+            t.hi = s_hi[w] > t.hi ? s_hi[w] : t.hi;
+        }
+        tile_sum[blockIdx.x] = t;
+    }
     if (threadIdx.x < world) tile_cnt[(size_t)blockIdx.x * world + threadIdx.x] = s_cnt[threadIdx.x];
 }
 
@@ -124,11 +132,36 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint6
 // + an exclusive prefix over tiles) into tile_off, and owner o's info row
 __global__ __launch_bounds__(RT_BLOCK) void k_route_scan(uint32_t tiles, uint32_t world,
                                                          const uint32_t* __restrict__ tile_cnt,
-                                                         uint32_t* __restrict__ tile_off, const PackSum* sum,
+                                                         uint32_t* __restrict__ tile_off,
+                                                         const PackSum* __restrict__ tile_sum,
                                                          int64_t* __restrict__ info) {
     __shared__ uint32_t s_tmp[RT_BLOCK / 64];
     __shared__ uint32_t s_run;
+    __shared__ unsigned long long s_lo[RT_BLOCK / 64], s_hi[RT_BLOCK / 64];
+    __shared__ uint32_t s_uns;
     const uint32_t o = blockIdx.x, tid = threadIdx.x;
+    // the batch summary from the tiles' summaries
+    unsigned long long lo = ~0ull, hi = 0;
+    uint32_t uns = 0;
+    for (uint32_t t = tid; t < tiles; t += RT_BLOCK) {
+        const PackSum ps = tile_sum[t];
+        lo = ps.lo < lo ? ps.lo : lo;
+        hi = ps.hi > hi ? ps.hi : hi;
+        uns |= ps.unsorted;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if (tid == 0) s_uns = 0;
+    __syncthreads();
+    if ((tid & 63) == 0) {
+        s_lo[tid >> 6] = lo;
+        s_hi[tid >> 6] = hi;
+    }
+    if (uns) s_uns = 1;   // benign race: every writer stores 1
+    __syncthreads();
     uint32_t part = 0;
     for (uint32_t k = tid; k < tiles * o; k += RT_BLOCK) part += tile_cnt[(size_t)(k / o) * world + (k % o)];
     for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
@@ -158,11 +191,15 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scan(uint32_t tiles, uint32_
         run += tot;
     }
     if (tid == 0) {
+        for (int w = 0; w < RT_BLOCK / 64; w++) {
+            lo = s_lo[w] < lo ? s_lo[w] : lo;
+            hi = s_hi[w] > hi ? s_hi[w] : hi;
+        }
         int64_t* row = info + (size_t)RL_ROUTE_INFO * o;
         row[0] = run - base;
-        row[1] = tiles ? unbias(sum->lo) : INT64_MAX;
-        row[2] = tiles ? unbias(sum->hi) : INT64_MIN;
-        row[3] = sum->unsorted ? 0 : 1;
+        row[1] = tiles ? unbias(lo) : INT64_MAX;
+        row[2] = tiles ? unbias(hi) : INT64_MIN;
+        row[3] = s_uns ? 0 : 1;
     }
 }
 
@@ -322,7 +359,7 @@ struct rl_router {
     uint32_t world = 1, max_batch = 0, max_recv = 0;
     uint32_t* tile_cnt = nullptr;    // pack: [tiles][world]
     uint32_t* tile_off = nullptr;    // pack: [tiles][world] output offsets
-    PackSum* psum = nullptr;         // pack: batch summary
+    PackSum* psum = nullptr;         // pack: per-tile summaries [tiles]
     uint32_t* ctrl = nullptr;        // merge: MC_* words + look-back status
     uint32_t* status = nullptr;      // merge: [MERGE_PASSES][tiles][RADIX]
     size_t ctrl_bytes = 0;
@@ -348,7 +385,7 @@ extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batc
     r->ctrl_bytes = 4 * (MC_WORDS + (size_t)MERGE_PASSES * stiles * RADIX);
     bool ok = hipMalloc(&r->tile_cnt, 4 * ptiles * world) == hipSuccess;
     ok = ok && hipMalloc(&r->tile_off, 4 * ptiles * world) == hipSuccess;
-    ok = ok && hipMalloc(&r->psum, sizeof(PackSum)) == hipSuccess;
+    ok = ok && hipMalloc(&r->psum, sizeof(PackSum) * (ptiles ? ptiles : 1)) == hipSuccess;
     ok = ok && hipMalloc(&r->ctrl, r->ctrl_bytes) == hipSuccess;
     for (uint32_t** p : {&r->k0, &r->k1, &r->v0, &r->v1}) ok = ok && hipMalloc(p, 4 * (size_t)max_recv) == hipSuccess;
     ok = ok && hipMalloc(&r->d_status, 4) == hipSuccess && hipMemset(r->d_status, 0, 4) == hipSuccess;
@@ -425,7 +462,6 @@ extern "C" int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const 
     (void)hipSetDevice(r->device);
     hipStream_t s = (hipStream_t)stream;
     const uint32_t tiles = (uint32_t)((m + RT_TILE - 1) / RT_TILE);
-    k_pack_init<<<1, 1, 0, s>>>(r->psum);
     if (m) k_route_hist<<<tiles, RT_BLOCK, 0, s>>>((uint32_t)m, key, ts, r->world, r->tile_cnt, r->psum);
     k_route_scan<<<r->world, RT_BLOCK, 0, s>>>(tiles, r->world, r->tile_cnt, r->tile_off, r->psum, send_info);
     if (!m) return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
