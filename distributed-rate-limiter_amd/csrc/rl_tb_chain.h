@@ -554,10 +554,17 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
         for (uint32_t b = 0; b < ne; b += 64) {
             const uint32_t g = b + lane;
             const bool v = g < ne;
-            uint32_t t = 0;
+            // the tile t holding near entry g and its first near index NPF[t]
+            // (NPF is non-decreasing; selects on wave-uniform values: indexing
+            // NPF by a lane-varying t made the compiler spill it to scratch)
+            uint32_t t = 0, base = NPF[0];
 #pragma unroll
-            for (int u = 1; u < CH_NP; u++) t += g >= NPF[u] ? 1u : 0u;
-            const uint32_t k = v ? g - pick(NPF, t) : 0u;
+            for (int u = 1; u < CH_NP; u++) {
+                const bool ge = g >= NPF[u];
+                t += ge ? 1u : 0u;
+                base = ge ? NPF[u] : base;
+            }
+            const uint32_t k = v ? g - base : 0u;
             const double pn = __shfl(tbase, (int)t) + sh.ne_pred[cb][t][k];
             const double ad = sh.ne_add[cb][t][k];
             const double th = sh.ne_th[cb][t][k];
