@@ -353,44 +353,156 @@ namespace rl {
 //   [2] heavy window segments (one thread each, dequeued before the light ones),
 //   [3] huge token-bucket segments (the chain dequeues these first: longest-first
 //       keeps one hot key from starting last).
-// One tile of SEG_TILE sorted positions per block; list slots are reserved
-// with ONE global atomic per list per block (a single contended word sustains
-// only ~88 atomics/us on MI355X).
-constexpr int SEG_ITEMS = 16;
+// One tile of SEG_TILE sorted positions per block, staged in LDS; thread t
+// takes the SEG_ITEMS consecutive positions of chunk t.  A segment ends at the
+// next head: inside the chunk, else at the first head of a later chunk (a
+// block suffix-min over the chunks' first heads), else past the tile -- at most
+// one head per tile (the tile's last), whose end one wave finds with a 64-ary
+// search (wave_seg_end: a few rounds of one load per lane instead of one
+// thread's dependent galloping).  List slots are reserved with ONE global
+// atomic per list per block (a single contended word sustains only ~88
+// atomics/us on MI355X).
+#ifndef RL_SEG_ITEMS
+#define RL_SEG_ITEMS 16
+#endif
+constexpr int SEG_ITEMS = RL_SEG_ITEMS;
 constexpr int SEG_TILE = 256 * SEG_ITEMS;
+constexpr uint32_t SEG_NONE = 0xffffffffu;
+
+// the first position e >= from with e == m or sk[e] != k0, every position in
+// [from0, from) holding k0; all 64 lanes call it with the same arguments
+__device__ inline uint32_t wave_seg_end(const uint32_t* __restrict__ sk, uint32_t m, uint32_t from, uint32_t k0) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t lo = from;
+    uint64_t step = 1;
+    for (int guard = 0; guard < 64; guard++) {
+        const uint64_t p = (uint64_t)lo + step * lane;
+        const bool diff = p >= m || sk[p] != k0;
+        const uint64_t b = __ballot(diff);
+        if (b) {
+            const uint32_t f = (uint32_t)__ffsll((unsigned long long)b) - 1;
+            if (step == 1 || f == 0) {
+                if (f == 0) return lo;
+                return lo + f;                            // step == 1
+            }
+            lo = (uint32_t)(lo + step * (f - 1) + 1);     // end in (p_{f-1}, p_f]
+            step = (step + 63) / 64;
+        } else {
+            lo = (uint32_t)(lo + step * 63 + 1);
+            step *= 64;
+        }
+    }
+    return m;   // unreachable (the step grows 64x per round)
+}
+
+__device__ inline uint32_t seg_skew(uint32_t i) { return i + (i >> 4); }   // LDS bank skew of a 16-element chunk
 
 __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ sk, uint32_t m,
                                                   uint32_t invalid_key, uint32_t win_base, uint32_t heavy_min,
                                                   uint32_t huge_min, SegLists L) {
-    __shared__ uint32_t s_cnt[4], s_base[4];
+    __shared__ uint32_t s_k[SEG_TILE + SEG_TILE / 16];
+    __shared__ uint32_t s_next[256];      // first head of chunk t, then of chunks > t
+    __shared__ uint32_t s_cnt[4], s_base[4], s_open, s_open_end;
+    __shared__ uint64_t s_wsum[4];
     const uint32_t tid = threadIdx.x;
     for (uint32_t tile = blockIdx.x; tile * SEG_TILE < m; tile += gridDim.x) {
-        if (tid < 4) s_cnt[tid] = 0;
+        const uint32_t t0 = tile * SEG_TILE;
+        const uint32_t n = min((uint32_t)SEG_TILE, m - t0);
+        if (tid == 0) s_open = SEG_NONE;
+#pragma unroll
+        for (int j = 0; j < SEG_ITEMS; j++) {   // coalesced
+            const uint32_t i = j * 256 + tid;
+            s_k[seg_skew(i)] = i < n ? sk[t0 + i] : invalid_key;
+        }
+        const uint32_t kprev = t0 > 0 ? sk[t0 - 1] : invalid_key;
         __syncthreads();
+        const uint32_t c0 = tid * SEG_ITEMS;
+        uint32_t key[SEG_ITEMS];
+        uint32_t hmask = 0;
+        uint32_t before = c0 == 0 ? kprev : s_k[seg_skew(c0 - 1)];
+#pragma unroll
+        for (int q = 0; q < SEG_ITEMS; q++) {
+            key[q] = s_k[seg_skew(c0 + q)];
+            const bool head = c0 + q < n && key[q] != invalid_key && key[q] != before;
+            hmask |= head ? 1u << q : 0u;
+            before = key[q];
+        }
+        // a chunk's first boundary for the segments before it: any head, or
+        // an invalid key (rejected requests end a segment too)
+        uint32_t bmask = hmask;
+#pragma unroll
+        for (int q = 0; q < SEG_ITEMS; q++)
+            if (c0 + q >= n || key[q] == invalid_key) bmask |= 1u << q;
+        s_next[tid] = bmask ? c0 + (uint32_t)__builtin_ctz(bmask) : SEG_NONE;
+        __syncthreads();
+        // suffix min over later chunks: s_next[t] = first boundary in chunks > t
+        for (uint32_t d = 1; d < 256; d <<= 1) {
+            const uint32_t v = tid + d < 256 ? s_next[tid + d] : SEG_NONE;
+            const uint32_t mine = s_next[tid];
+            __syncthreads();
+            s_next[tid] = min(mine, v);
+            __syncthreads();
+        }
+        // (s_next[t] now = min over chunks >= t; the boundary after chunk t is s_next[t + 1])
+        const uint32_t after = tid + 1 < 256 ? s_next[tid + 1] : SEG_NONE;
         SegRec rec[SEG_ITEMS];
         uint32_t slot[SEG_ITEMS];
 #pragma unroll
-        for (int j = 0; j < SEG_ITEMS; j++) {
-            uint32_t i = tile * SEG_TILE + j * 256 + tid;
-            slot[j] = 0xffffffffu;
-            if (i >= m) continue;
-            uint32_t k = sk[i];
-            bool head = k != invalid_key && (i == 0 || sk[i - 1] != k);
-            if (!head) continue;
-            uint32_t len = seg_end(sk, m, i, k) - i;
-            rec[j] = SegRec{i, len};
-            const bool tb = k < win_base;
+        for (int q = 0; q < SEG_ITEMS; q++) {
+            slot[q] = 0xffffffffu;
+            if (!((hmask >> q) & 1u)) continue;
+            const uint32_t later = bmask & ~((2u << q) - 1u);   // boundaries after q in the chunk
+            const uint32_t e = later ? c0 + (uint32_t)__builtin_ctz(later) : after;
+            rec[q] = SegRec{t0 + c0 + q, e == SEG_NONE ? 0u : e - (c0 + q)};
+            if (e == SEG_NONE) s_open = c0 + q;                 // the tile's last head: its end is past the tile
+        }
+        __syncthreads();
+        if (s_open != SEG_NONE && tid < 64) {
+            const uint32_t o = s_open;
+            const uint32_t e = wave_seg_end(sk, m, t0 + n, s_k[seg_skew(o)]);
+            if (tid == 0) s_open_end = e;
+        }
+        __syncthreads();
+        // list slots in position order (a block scan of the per-chunk counts,
+        // four 16-bit fields): light segments then replay with neighbouring
+        // threads on neighbouring positions (coalesced)
+        uint64_t cnt4 = 0;
+#pragma unroll
+        for (int q = 0; q < SEG_ITEMS; q++) {
+            if (!((hmask >> q) & 1u)) continue;
+            if (c0 + q == s_open) rec[q].len = s_open_end - (t0 + c0 + q);
+            const uint32_t len = rec[q].len;
+            const bool tb = key[q] < win_base;
             const uint32_t which = len < heavy_min ? 1u : !tb ? 2u : len >= huge_min ? 3u : 0u;
-            slot[j] = (which << 30) | atomicAdd(&s_cnt[which], 1u);
+            slot[q] = (which << 30) | (uint32_t)((cnt4 >> (16 * which)) & 0xffffu);
+            cnt4 += 1ull << (16 * which);
+        }
+        const uint64_t inc = wave_incl_scan_i64((int64_t)cnt4);
+        if ((tid & 63) == 63) s_wsum[tid >> 6] = inc;
+        __syncthreads();
+        uint64_t exc = inc - cnt4;
+        for (uint32_t w = 0; w < (tid >> 6); w++) exc += s_wsum[w];
+        if (tid == 255) {
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint32_t tot = (uint32_t)(((exc + cnt4) >> (16 * w)) & 0xffffu);   // block total per list
+                s_cnt[w] = tot;
+            }
         }
         __syncthreads();
         if (tid < 4) s_base[tid] = s_cnt[tid] ? atomicAdd(&L.count[tid], s_cnt[tid]) : 0u;
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < SEG_ITEMS; j++) {
-            if (slot[j] == 0xffffffffu) continue;
-            const uint32_t which = slot[j] >> 30, off = slot[j] & 0x3fffffffu;
-            L.list[which][s_base[which] + off] = rec[j];
+        for (int q = 0; q < SEG_ITEMS; q++) {
+            if (slot[q] == 0xffffffffu) continue;
+            const uint32_t which = slot[q] >> 30;
+            slot[q] += (uint32_t)((exc >> (16 * which)) & 0xffffu);
+        }
+#pragma unroll
+        for (int q = 0; q < SEG_ITEMS; q++) {
+            if (slot[q] == 0xffffffffu) continue;
+            const uint32_t which = slot[q] >> 30, off = slot[q] & 0x3fffffffu;
+            L.list[which][s_base[which] + off] = rec[q];
         }
         __syncthreads();
     }

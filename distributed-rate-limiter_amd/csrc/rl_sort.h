@@ -24,7 +24,10 @@
 namespace rl {
 
 constexpr int SORT_BLOCK = 256;
-constexpr int SORT_ITEMS = 16;
+#ifndef RL_SORT_ITEMS
+#define RL_SORT_ITEMS 16
+#endif
+constexpr int SORT_ITEMS = RL_SORT_ITEMS;   // keys per thread; a tile is SORT_BLOCK x SORT_ITEMS
 constexpr int SORT_TILE = SORT_BLOCK * SORT_ITEMS;
 constexpr int SORT_WAVES = SORT_BLOCK / 64;
 constexpr int RADIX = 256;

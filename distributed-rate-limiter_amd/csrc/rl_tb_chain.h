@@ -68,15 +68,29 @@ constexpr int CH_NE = 64;                              // near-list capacity per
 // with the mostly idle loader (wave 4) and the producers pair up on the
 // other three SIMDs.
 constexpr int CH_LOADER = 4;
-static_assert(CH_NP + 2 <= 16 && CH_NP >= 3, "wave roles");
+// RL_CH_IDLE: wave 8 (the chain's SIMD again) takes no work, so no producer
+// competes with the chain wave for that SIMD's issue slots
+#ifndef RL_CH_IDLE
+#define RL_CH_IDLE 0
+#endif
+constexpr int CH_IDLE = RL_CH_IDLE ? 8 : -1;
+static_assert(CH_NP + 2 + (RL_CH_IDLE ? 1 : 0) <= 16 && CH_NP >= 3 && (!RL_CH_IDLE || CH_NP >= 7), "wave roles");
 __device__ inline int ch_producer_index(uint32_t wave) {
-    return wave == 0 || wave == (uint32_t)CH_LOADER ? -1 : (int)wave - (wave < (uint32_t)CH_LOADER ? 1 : 2);
+    if (wave == 0 || wave == (uint32_t)CH_LOADER || (int)wave == CH_IDLE) return -1;
+    return (int)wave - (wave < (uint32_t)CH_LOADER ? 1 : 2) - ((CH_IDLE >= 0 && (int)wave > CH_IDLE) ? 1 : 0);
 }
-constexpr int CH_BLOCK = (CH_NP + 2) * 64;
+constexpr int CH_BLOCK = (CH_NP + 2 + (RL_CH_IDLE ? 1 : 0)) * 64;
 #ifndef RL_CH_SERIAL
 #define RL_CH_SERIAL 64
 #endif
 constexpr int CH_SERIAL = RL_CH_SERIAL;                // serial exact steps per round at most
+// serial steps go on until CH_LINGER steps past the last one that left the
+// regime: regime exits come in clusters (a balance random-walking across a
+// decade boundary or zero), and a serial step costs ~1/18 of a round
+#ifndef RL_CH_LINGER
+#define RL_CH_LINGER 0
+#endif
+constexpr uint32_t CH_LINGER = RL_CH_LINGER;
 // conservative scale of the allow/clamp threshold th*P (covers the rounding of
 // th*P and of the bound arithmetic with a wide margin)
 constexpr double CH_YSCALE = 1.0 - 0x1p-28;
@@ -717,8 +731,8 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     // arithmetic, not a dependent memory round trip
     int64_t nvec = 0;
     double avec = 0.0, capvec = 0.0;
-    uint32_t k = 0;
-    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
+    uint32_t k = 0, kx = 0;   // kx: steps done when the last regime exit happened
+    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE || k < kx + CH_LINGER); k++) {
         if ((k & 63u) == 0) {
             const uint32_t pq = q + lane;
             nvec = pq < j1 ? a.n[pq] : 1;
@@ -733,7 +747,8 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
         const TbEval v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
         if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
         force = v.allowed || v.clamped || !alive;
-        if (emode != QM_NONE && v.inrange) {
+        const bool same = emode != QM_NONE && v.inrange;
+        if (same) {
             D = v.Dact;                     // same decade / binade (sign may flip)
         } else {
             const TbQ nq = tb_quant(v.tokens, profile);
@@ -742,7 +757,9 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
             emode = fast_mode(D < 0 ? -D : D, E, profile);
             if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
         }
+        const bool was_fast = mode != QM_NONE;
         mode = fast_mode(D, E, profile);
+        if (force || mode == QM_NONE || !was_fast || !same) kx = k + 1;   // this step left the regime
         q++;
     }
     return SerialOut{q, D, E, mode, k};
@@ -1025,6 +1042,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             CH_T(t1);
             cyc[0] += t1 - t0;
+        } else if ((int)wave == CH_IDLE) {
+            // no work: only the round barrier
         } else if (wave == (uint32_t)CH_LOADER) {
             const uint32_t first = s.ccnt ? s.cfirst : s.pfirst;
             ld_until(L, sh, first, s.pfirst + 2 * CH_W, j1, pre, lane);

@@ -1,0 +1,7 @@
+#!/bin/bash
+# A/B of the chain's serial linger (make variant builds) on the hot-key workloads
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+V="librl_amd_base.so librl_amd.so librl_amd_l8.so librl_amd_l16.so librl_amd_l32s256.so librl_amd_s256.so"
+BARGS="--lat-batches 0" STEPS=12 bash scripts/ab.sh $V || exit $?
+BARGS="--workload tb_zipf15 --lat-batches 0" STEPS=8 bash scripts/ab.sh $V || exit $?
+BARGS="--workload tb_hot --lat-batches 0" STEPS=4 bash scripts/ab.sh librl_amd.so librl_amd_l16.so librl_amd_l32s256.so || exit $?

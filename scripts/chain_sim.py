@@ -185,5 +185,92 @@ def main():
           f"<64: {(gaps < 64).sum()}, >=2240: {(gaps >= 2240).sum()}")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not (len(sys.argv) > 1 and sys.argv[1] == "exits"):
     main()
+
+
+def exit_trace(s, nkeys, nb):
+    """exact replay of the hottest key: per step (exit?, state positive after?)"""
+    gen = traces.TokenBucketZipf(nkeys=nkeys, s=s)
+    rate, cap = 20 / 12.0, 20.0
+    tok_q, last_q = cap, None
+    ex, pos = [], []
+    hot = None
+    for _ in range(nb):
+        k, t, _, _ = gen.next_batch()
+        if hot is None:
+            vals, cnt = np.unique(k, return_counts=True)
+            hot = vals[np.argmax(cnt)]
+        for tt in t[k == hot]:
+            now = float(int(tt)) / 1e9
+            add = 0.0 if last_q is None else (now - last_q) * rate
+            ssum = tok_q + add
+            tok = ssum if ssum < cap else cap
+            allowed = tok >= 1.0
+            if allowed:
+                tok -= 1.0
+            nq = q14(tok)
+            e_old = dec_of(tok_q)[1] if tok_q > 0 else None
+            e_new = dec_of(nq)[1] if nq > 0 else None
+            ex.append(allowed or ssum >= cap or tok_q <= 0 or nq <= 0 or e_old != e_new)
+            pos.append(nq > 0)
+            tok_q, last_q = nq, q14(now)
+    return np.array(ex), np.array(pos)
+
+
+def round_model(ex, pos, W=2240, serial_cap=64, linger=0):
+    """rounds and serial steps of the chain's round structure (approximation of
+    ch_segment): a full window costs one round; a window with a regime exit
+    costs its round, exact serial steps from the exit, and a producers-only
+    round for the next window.  Serial steps go on while the last step left
+    the regime or the state is not positive (and, with `linger`, until
+    `linger` steps past the last exit), at most serial_cap per round."""
+    N = ex.size
+    rounds = 1                       # first window
+    serial = stops = 0
+    p = 0
+    while p < N:
+        rounds += 1
+        hit = np.flatnonzero(ex[p:p + W])
+        if hit.size == 0:
+            p += W
+            continue
+        stops += 1
+        q = p + int(hit[0])
+        k = 0
+        last = q
+        while q < N and k < serial_cap:
+            need = k == 0 or ex[q - 1] or not pos[q - 1] or q - last < linger
+            if not need:
+                break
+            if ex[q]:
+                last = q
+            q += 1
+            k += 1
+        serial += k
+        p = q
+        rounds += 1                  # producers-only round for the next window
+    return rounds, serial, stops
+
+
+def exits_main(argv):
+    s = float(argv[0])
+    nkeys = int(argv[1])
+    nb = int(argv[2]) if len(argv) > 2 else 1
+    ex, pos = exit_trace(s, nkeys, nb + 1)
+    n0 = int(np.ceil(ex.size / (nb + 1)))     # skip the first batch (the bucket starts full)
+    ex, pos = ex[n0:], pos[n0:]
+    N = ex.size
+    idx = np.flatnonzero(ex)
+    gaps = np.diff(idx)
+    print(f"s={s} nkeys={nkeys}: {N} hot steps over {nb} batches, exits {idx.size} ({idx.size / nb:.0f}/batch); "
+          f"gaps <8: {(gaps < 8).sum()} <32: {(gaps < 32).sum()} <128: {(gaps < 128).sum()} <1024: {(gaps < 1024).sum()}")
+    for linger in (0, 16, 32, 64, 128):
+        for cap in (64, 256):
+            r, se, st = round_model(ex, pos, serial_cap=cap, linger=linger)
+            print(f"  linger {linger:4d} cap {cap:4d}: rounds {r / nb:7.1f}/batch serial {se / nb:8.1f}/batch "
+                  f"stops {st / nb:6.1f}  model cycles/batch {(r * 8000 + se * 440) / nb / 1e3:8.0f}k")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "exits":
+    exits_main(sys.argv[2:])
