@@ -929,10 +929,17 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
                                                             B.runs);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 19);
     if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 3);
-    if (e->timing) (void)hipEventRecord(ev[5], c);
-    HIPCHK(e, hipEventRecord(B.chain_done, c));
+    // the replay's end: with timing on, its timing event also orders the
+    // finish stream (one marker packet on the chain stream instead of two)
+    hipEvent_t chain_end = B.chain_done;
+    if (e->timing) {
+        HIPCHK(e, hipEventRecord(ev[5], c));
+        chain_end = ev[5];
+    } else {
+        HIPCHK(e, hipEventRecord(B.chain_done, c));
+    }
     // finish: outputs of the committed runs, results to the caller's order
-    HIPCHK(e, hipStreamWaitEvent(t, B.chain_done, 0));
+    HIPCHK(e, hipStreamWaitEvent(t, chain_end, 0));
     if (tall) (void)hipEventRecord(ev[6], t);
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 4);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
