@@ -261,6 +261,16 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
     const double p = x * P;
     const double err = __builtin_fma(x, P, -p);       // x*P == p + err exactly
     ge_lo = (p > (double)DEC_LO) | ((p == (double)DEC_LO) & (err >= 0.0));
+#if RL_STEP_RINT
+    // RNE of p, then the exact product decides a tie of p: p - rint(p) is
+    // +-1/2 exactly only when p's fraction is 1/2 (p < 2^52 has ulp <= 1/2),
+    // and |err| <= ulp(p)/2 cannot move a non-tie across the half
+    double d = rint(p);
+    const double h = p - d;                           // exact
+    d += ((h == 0.5) & (err > 0.0)) ? 1.0 : 0.0;
+    d -= ((h == -0.5) & (err < 0.0)) ? 1.0 : 0.0;
+    return d;
+#endif
     const double d0 = floor(p);
     const double f = p - d0;                          // exact
     const bool odd = d0 * 0.5 != floor(d0 * 0.5);
@@ -276,7 +286,10 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
 // the decade, or an expired key (add NaN).
 template <int MODE>
 __device__ inline double tb_step_d(double Dpred, double P, double R, double add, double th, double& tokens) {
-    const double T = MODE == QM_DEC ? rlq::div_pow10(Dpred, P, R)   // strtod("D e(E-13)")
+    // strtod("D e(E-13)"): D < 2^47 and P = 10^k (k <= 22) are exact doubles,
+    // so one correctly rounded IEEE division is strtod's result (Clinger's
+    // fast path); div_pow10 reaches the same value through a corrected product
+    const double T = MODE == QM_DEC ? (RL_STEP_DIV ? Dpred / P : rlq::div_pow10(Dpred, P, R))
                                     : Dpred * R;                    // exact: R = 2^E
     const double sum = T + add;
     tokens = sum;
