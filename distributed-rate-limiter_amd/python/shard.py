@@ -133,6 +133,12 @@ class RoutedPipeline:
             )
             self.slots.append(s)
         self.last_recv = 0
+        # the merge on the batch's own stream S instead of R: R then carries
+        # only packs and exchanges, so the count copies later batches wait for
+        # are not queued behind merges; merges stay in step order (the router's
+        # scratch and store clock) through ev_last_merge
+        self.merge_on_s = self.cuda and not os.environ.get("RL_ROUTE_MERGE_ON_R")
+        self.ev_last_merge = None
         self.wait_s = 0.0          # host time spent waiting for count copies
         self.host_prof = {}
 
@@ -202,11 +208,15 @@ class RoutedPipeline:
         assert tot <= self.max_recv, "received more than max_recv"
         self.last_recv = tot
         p = self._p
+        def merge(stream):
+            self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]),
+                           p(s["sms"]), p(s["at"]), self._sp(stream))
+
         with _ctx(self.R):
             self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
             self._tick("b_a2a_req")
-            self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]),
-                           p(s["sms"]), p(s["at"]), self._sp(self.R))
+            if not self.merge_on_s:
+                merge(self.R)
             if self.cuda:
                 s["ev_merged"] = torch.cuda.Event()
                 s["ev_merged"].record(self.R)
@@ -215,6 +225,12 @@ class RoutedPipeline:
         with _ctx(S):
             if S is not None:
                 S.wait_event(s["ev_merged"])
+            if self.merge_on_s:
+                if self.ev_last_merge is not None:
+                    S.wait_event(self.ev_last_merge)
+                merge(S)
+                self.ev_last_merge = torch.cuda.Event()
+                self.ev_last_merge.record(S)
             self.decide(tot, p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]), p(s["sms"]), p(s["dec"]),
                         p(s["rem"]), p(s["retry"]), p(s["reset"]), self._sp(S))
             self._tick("b_decide")

@@ -168,6 +168,28 @@ def test_chain_regimes(rl, profile, kind):
     run_both(rl, profile, configs, split(_chain_trace(kind, seed), [50_000, 70_000]))
 
 
+@pytest.mark.parametrize("counts", [
+    [4096, 4095, 4097, 1, 8191, 8192, 1, 2, 3, 4094, 1, 4096],     # boundaries at and around tile edges
+    [4096] * 6,                                                   # m a multiple of the tile: no tail positions
+    [1] * 5000 + [20_000, 3, 12_289],                             # many heads per chunk, then segments past tiles
+])
+def test_segment_tile_boundaries(rl, counts):
+    # k_segments stages 4096-position tiles: segments starting / ending exactly
+    # at, one before and one after a tile edge, a segment running over several
+    # tiles to the batch end, and rejected requests (n = 0, sorted last)
+    configs = CONFIG_SETS["mixed"]
+    rng = np.random.default_rng(len(counts))
+    key = np.concatenate([np.full(c, 1000 + i, np.uint64) for i, c in enumerate(counts)])
+    key = key[rng.permutation(key.size)]
+    m = key.size
+    ts = T0 + np.cumsum(rng.integers(0, 400_000, m)).astype(np.int64)
+    n = np.ones(m, np.int64)
+    if m % 4096:
+        n[rng.random(m) < 0.01] = 0
+    cfg = (key % len(configs)).astype(np.uint32)
+    run_both(rl, 0, configs, split((key, ts, n, cfg, None), [m]))
+
+
 def test_single_hot_key_full_batch(rl):
     # the bench's diagnostic workload: one key carries the whole 1M batch
     g = traces.TokenBucketZipf(nkeys=1, batch=1_000_000)
