@@ -82,11 +82,16 @@ class RoutedPipeline:
     (include/rl_route.h), the same on every owner."""
 
     def __init__(self, ops, decide, world, max_batch, device, pg_req=None, pg_res=None, depth=6, lookahead=2,
-                 max_recv=None, staged=False):
+                 max_recv=None, staged=False, pg_cnt=None):
         self.ops, self.decide, self.world = ops, decide, world
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
         self.pg_req, self.pg_res = pg_req, pg_res
+        # pg_cnt (optional): a process group of its own for the packs' count
+        # exchange, on a stream of its own (C): a batch's counts then never
+        # queue behind earlier batches' record exchanges, and the host, which
+        # needs them for the split sizes, finds them ready
+        self.pg_cnt = pg_cnt
         self.depth, self.lookahead = depth, lookahead
         self.staged = staged          # all-to-alls through host memory (gloo with device tensors)
         mb = max_batch
@@ -106,6 +111,7 @@ class RoutedPipeline:
             return mk() if mk is not None else torch.cuda.Stream(d)
 
         self.R = new_stream()
+        self.C = new_stream() if pg_cnt is not None else self.R
         self.slots = []
         for _ in range(depth):
             s = dict(
@@ -177,19 +183,20 @@ class RoutedPipeline:
         s["m"], s["busy"] = m, True
         p = self._p
         self._tick(None)
-        with _ctx(self.R):
+        C = self.C
+        with _ctx(C):
             if s["ev_done"] is not None:
-                self.R.wait_event(s["ev_done"])   # the set's previous batch has finished
+                C.wait_event(s["ev_done"])   # the set's previous batch has finished
             self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]),
-                          self._sp(self.R))
+                          self._sp(C))
             self._tick("a_pack")
-            self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_req)
+            self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_cnt if self.pg_cnt is not None else self.pg_req)
             self._tick("a_a2a_cnt")
             s["cnt_h"][0].copy_(s["scnt"], non_blocking=True)
             s["cnt_h"][1].copy_(s["rcnt"], non_blocking=True)
             if self.cuda:
                 s["ev_cnt"] = torch.cuda.Event()
-                s["ev_cnt"].record(self.R)
+                s["ev_cnt"].record(C)
 
     def stage_b(self, b, dec, rem, retry, reset):
         """move batch b's requests, decide them at their owners, bring the
@@ -213,6 +220,8 @@ class RoutedPipeline:
                            p(s["sms"]), p(s["at"]), self._sp(stream))
 
         with _ctx(self.R):
+            if self.C is not self.R:
+                self.R.wait_event(s["ev_cnt"])    # the pack (send, rcnt) is complete
             self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
             self._tick("b_a2a_req")
             if not self.merge_on_s:
