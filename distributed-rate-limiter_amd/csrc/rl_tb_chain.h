@@ -314,7 +314,7 @@ __device__ inline int32_t fast_mode(int64_t D, int32_t E, int32_t profile) {
 __device__ inline void mode_scale(int32_t mode, int32_t E, double& P, double& R) {
     if (mode == QM_DEC) {
         P = rlq::pow10_exact(13 - E);
-        R = 1.0 / P;
+        R = RL_STEP_DIV ? 0.0 : 1.0 / P;   // the division step (RL_STEP_DIV) needs no reciprocal
     } else {
         P = ldexp(1.0, -E);
         R = ldexp(1.0, E);
@@ -723,8 +723,8 @@ struct SerialOut {
     uint32_t steps;
 };
 
-template <typename AddAt>
-__device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt add_at, uint32_t q, int64_t D, int32_t E,
+template <typename AddAt, typename ThAt>
+__device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt add_at, ThAt th_at, uint32_t q, int64_t D, int32_t E,
                                                                        bool force, uint32_t lim, uint32_t j1,
                                                                        const CfgDev* __restrict__ cfgs,
                                                                        int32_t profile, const ReqArgs& a) {
@@ -739,25 +739,30 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     int32_t emode = fast_mode(D < 0 ? -D : D, E, profile);
     double Ps = 1.0, Rs = 1.0;
     if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
-    // every input of the next 64 positions in one vector load each (lane k holds
-    // position q + k): the steps below read registers only, so a step costs its
-    // arithmetic, not a dependent memory round trip
-    int64_t nvec = 0;
-    double avec = 0.0, capvec = 0.0;
+    // add and th = min(capacity, n) of the next 64 positions in one vector load
+    // each (lane k holds position q + k; the chain's are in its LDS ring): a
+    // step costs its arithmetic, not a dependent memory round trip.  n and the
+    // capacity themselves matter only when sum >= th (an allow or a clamp) or
+    // the key has expired: below th the step denies without clamping whatever
+    // they are, so only those steps load them (from HBM)
+    double avec = 0.0, tvec = 0.0;
     uint32_t k = 0, kx = 0;   // kx: steps done when the last regime exit happened
     for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE || k < kx + CH_LINGER); k++) {
         if ((k & 63u) == 0) {
             const uint32_t pq = q + lane;
-            nvec = pq < j1 ? a.n[pq] : 1;
             avec = pq < lim ? add_at(pq) : 0.0;
-            capvec = cfgs[pq < j1 ? a.cfg[pq] : 0u].limit_d;
+            tvec = pq < lim ? th_at(pq) : 0.0;
         }
         const uint32_t kl = k & 63u;
         const double add = __longlong_as_double(readlane_i64(__double_as_longlong(avec), kl));
         const bool alive = add == add;
-        const int64_t nn = readlane_i64(nvec, kl);
-        const double cap = __longlong_as_double(readlane_i64(__double_as_longlong(capvec), kl));
-        const TbEval v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
+        const double th = __longlong_as_double(readlane_i64(__double_as_longlong(tvec), kl));
+        TbEval v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, th, th, profile);
+        if (!alive || v.clamped) {      // sum >= th or an expired key: the real n and capacity
+            const int64_t nn = a.n[q];
+            const double cap = cfgs[a.cfg[q]].limit_d;
+            v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
+        }
         if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
         force = v.allowed || v.clamped || !alive;
         const bool same = emode != QM_NONE && v.inrange;
@@ -822,7 +827,8 @@ __device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, u
             pos += (uint32_t)__builtin_amdgcn_readfirstlane((int)brk);
             if (brk == len) continue;
         }
-        const SerialOut so = serial_steps([&](uint32_t p) { return src.add(p); }, pos, D, E, true, j1, j1, cfgs,
+        const SerialOut so = serial_steps([&](uint32_t p) { return src.add(p); }, [&](uint32_t p) { return src.th(p); },
+                                          pos, D, E, true, j1, j1, cfgs,
                                           profile, a);
         // wave-uniform by construction; say so (the loop and its ballots stay uniform)
         pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)so.q);
@@ -1098,7 +1104,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 // exact serial steps: the exiting step, then on while the state
                 // is off the fast decades or the last step left the regime
                 const uint32_t lim = (j1 - s.pfirst) < CH_W ? j1 : s.pfirst + CH_W;   // resident in the ring
-                const SerialOut so = serial_steps([&](uint32_t p) { return ring_add(sh, p); }, o.q, o.D, s.E, force,
+                const SerialOut so = serial_steps([&](uint32_t p) { return ring_add(sh, p); },
+                                                  [&](uint32_t p) { return ring_th(sh, p); }, o.q, o.D, s.E, force,
                                                   lim, j1, cfgs, profile, a);
                 nserial += so.steps;
                 CH_T(t1);
