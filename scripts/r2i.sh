@@ -3,4 +3,4 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 bash scripts/gpu_check.sh || exit $?
 grep -q " passed" gpurun_out/gpu_tests.log && ! grep -qE "[0-9]+ failed" gpurun_out/gpu_tests.log || { echo TESTS-FAILED; exit 1; }
-TAG=r2i bash scripts/profile.sh || exit $?
+TAG=${TAG:-r2i} bash scripts/profile.sh || exit $?
