@@ -167,6 +167,18 @@ __device__ inline double readlane_f64(double v, uint32_t l) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), (int)l);
     return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
+// max / min of two doubles that are never NaN: one v_max_f64 / v_min_f64 (the
+// compiler's fmax/fmin canonicalize both inputs first, three instructions)
+__device__ inline double vmax_f64(double a, double b) {
+    double r;
+    __asm__ volatile("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));   // volatile: never sunk into a branch
+    return r;
+}
+__device__ inline double vmin_f64(double a, double b) {
+    double r;
+    __asm__ volatile("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 template <typename Op>
 __device__ inline double wave_reduce_f64(double v, double ident, Op op) {
     v = op(v, dpp_f64<0x111, 0xf>(v, ident));
@@ -451,37 +463,41 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     double add[K], th[K], cb[K];
     double cum = 0.0, ymin = __builtin_inf(), cmax = -__builtin_inf(), cmin = __builtin_inf();
     uint32_t nearm = 0, evq = NO_STOP;
+    // branch-free: every ring slot is readable (positions past the window
+    // read stale slots, masked by v), and the bounds use v_max / v_min on
+    // values that are never NaN (no canonicalization)
 #pragma unroll
     for (int q = 0; q < K; q++) {
         const bool v = (uint32_t)q < nv;
-        const double a = v ? ring_add(sh, i0 + q) : 0.0;
+        const double araw = ring_add(sh, i0 + q);
         const double h = ring_th(sh, i0 + q);
+        const double a = v ? araw : 0.0;
         add[q] = a;
         th[q] = h;
         cb[q] = cum;
         const double pr = a * P;
         const bool ok = fabs(pr) < 0x1p49;                 // else NaN (expired key) or huge: a stop
-        if (!ok && evq == NO_STOP) evq = q;
-        const double rr = rint(pr);
+        evq = (!ok && evq == NO_STOP) ? (uint32_t)q : evq;
+        const double prs = ok ? pr : 0.0;                  // rint on every lane (no branch)
+        const double rr = rint(prs);
         if (MODE == QM_DEC) {
-            const double fr = (pr - rr) + __builtin_fma(a, P, -pr);   // a*P - rr, one rounding
-            if (ok && fabs(fr) > lim) nearm |= 1u << q;
-        } else if (ok && fabs(pr - rr) == 0.5) {                     // exact tie: parity decides
-            nearm |= 1u << q;
+            const double fr = (prs - rr) + __builtin_fma(a, P, -pr);  // a*P - rr, one rounding (ok lanes)
+            nearm |= (ok && fabs(fr) > lim) ? 1u << q : 0u;
+        } else {
+            nearm |= (ok && fabs(prs - rr) == 0.5) ? 1u << q : 0u;   // exact tie: parity decides
         }
-        cum += ok ? rr : 0.0;                                         // exact: |cum| < 2^52
-        if (v) {
-            cmax = fmax(cmax, cum);
-            cmin = fmin(cmin, cum);
-            ymin = fmin(ymin, h * PY - cum);
-        }
+        cum += rr;                                                    // exact: |cum| < 2^52
+        const double mx = vmax_f64(cmax, cum), mn = vmin_f64(cmin, cum), ym = vmin_f64(ymin, h * PY - cum);
+        cmax = v ? mx : cmax;
+        cmin = v ? mn : cmin;
+        ymin = v ? ym : ymin;
     }
     const int64_t Si = (int64_t)cum;
     const int64_t incl = wave_incl_scan_i64(Si);
     const double ex = (double)(incl - Si);
-    const double ymin_t = wave_reduce_f64(ymin - ex, __builtin_inf(), [](double x, double y) { return fmin(x, y); });
-    const double cmax_t = wave_reduce_f64(ex + cmax, -__builtin_inf(), [](double x, double y) { return fmax(x, y); });
-    const double cmin_t = wave_reduce_f64(ex + cmin, __builtin_inf(), [](double x, double y) { return fmin(x, y); });
+    const double ymin_t = wave_reduce_f64(ymin - ex, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
+    const double cmax_t = wave_reduce_f64(ex + cmax, -__builtin_inf(), [](double x, double y) { return vmax_f64(x, y); });
+    const double cmin_t = wave_reduce_f64(ex + cmin, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
     const uint32_t ev_t = wave_min_u32(evq != NO_STOP ? lane * K + evq : NO_STOP);
     const uint32_t ncnt = (uint32_t)__popc(nearm);
     const uint32_t ninc = wave_scan_u32(ncnt, 0u, [](uint32_t x, uint32_t y) { return x + y; });
