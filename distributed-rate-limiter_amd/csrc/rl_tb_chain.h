@@ -392,22 +392,22 @@ __device__ __attribute__((always_inline)) inline uint32_t exact_span(const Src& 
         }
         double D = (double)st, Db = 0.0;
         uint32_t bq = NO_STOP;
+        // every lane evaluates every step (selects, no branches): a lane past
+        // its steps or its first regime exit keeps its state
 #pragma unroll
         for (int q = 0; q < K; q++) {
-            if ((uint32_t)q < nv && bq == NO_STOP) {
-                double tk;
-                const double Dn = tb_step_d<MODE>(D, P, R, add[q], th[q], tk);
-                if (!(Dn == Dn)) {
-                    bq = q;
-                    Db = D;
-                } else {
-                    if (OUT) {
-                        a.tok[p + off + q] = tk;
-                        a.dec[p + off + q] = DEC_DENIED;
-                    }
-                    D = Dn;
-                }
+            const bool act = (uint32_t)q < nv && bq == NO_STOP;
+            double tk;
+            const double Dn = tb_step_d<MODE>(D, P, R, add[q], th[q], tk);
+            const bool stop = act && !(Dn == Dn);
+            const bool take = act && !stop;
+            bq = stop ? (uint32_t)q : bq;
+            Db = stop ? D : Db;
+            if (OUT && take) {
+                a.tok[p + off + q] = tk;
+                a.dec[p + off + q] = DEC_DENIED;
             }
+            D = take ? Dn : D;
         }
         const bool brk = bq != NO_STOP;
         const int64_t A = brk ? 0 : (int64_t)D - st;
