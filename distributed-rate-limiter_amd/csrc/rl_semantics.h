@@ -95,12 +95,16 @@ RL_HD inline int64_t floor_div(int64_t a, int64_t b) {
 
 // now.Truncate(W).Unix() (fixedwindow.go:72, slidingwindow.go:74); Truncate is
 // relative to Jan 1 year 1, hence the precomputed off_mod.
-RL_HD inline int64_t window_start(int64_t t, const CfgDev& c) {
+// the window's start in Unix ns: time.Truncate(t, W) (relative to year 1)
+RL_HD inline int64_t window_start_ns(int64_t t, const CfgDev& c) {
     int64_t tm = t % c.window;
     if (tm < 0) tm += c.window;
     int64_t r = tm + c.off_mod;
     if (r >= c.window) r -= c.window;
-    return floor_div(t - r, NS_PER_S);
+    return t - r;
+}
+RL_HD inline int64_t window_start(int64_t t, const CfgDev& c) {
+    return floor_div(window_start_ns(t, c), NS_PER_S);
 }
 
 // Redis 7 keyIsExpired(): now > when.  miniredis: a key is gone once its

@@ -894,7 +894,8 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
         const Out o0 = sw ? sw_step(w, S, r0.t, r0.n, r0.sms, C, profile, ef)
                           : fw_step(w, S, r0.t, r0.n, r0.sms, C, profile, ef);
         if (lane == 0) write_out(a, pos, o0);
-        const int64_t ws = window_start(r0.t, C), pws = ws - C.ttl_c;
+        const int64_t wsn = window_start_ns(r0.t, C);
+        const int64_t ws = floor_div(wsn, NS_PER_S), pws = ws - C.ttl_c;
         int ck = -1, pk = -1;
         for (int k = 0; k < 2; k++) {
             if (w.s[k].when == ABSENT) continue;
@@ -924,7 +925,11 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
                 t[q] = v ? a.ts[j] : 0;
                 n[q] = v ? a.n[j] : 0;
                 sm[q] = v ? a.sms[j] : 0;
-                same[q] = v && a.cfg[j] == c0 && window_start(t[q], C) == ws;
+                // window_start(t) == ws without two 64-bit divisions: W >= 1 s
+                // here (ttl_c > 0), so windows whose starts differ also differ
+                // in the key's second, and t is in r0's window iff it lies in
+                // [wsn, wsn + W)
+                same[q] = v && a.cfg[j] == c0 && t[q] >= wsn && t[q] - wsn < C.window;
                 if (v && !same[q] && firstx == NO_STOP) firstx = off + q;
             }
             const uint32_t cend = wave_min_u32(firstx);            // run end in this chunk (relative)
