@@ -249,16 +249,35 @@ __device__ __attribute__((always_inline)) inline void ld_issue(TbLoader& L, Chai
     }
 }
 
-// make [.., target) resident: issue what is missing and wait for everything
+// at most ~k LDS-DMA ops of this wave still in flight (k rounded down to a
+// waitcnt immediate)
+__device__ __attribute__((always_inline)) inline void ld_wait_at_most(uint32_t k) {
+    if (k >= 48u) __asm__ volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (k >= 32u) __asm__ volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (k >= 16u) __asm__ volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (k >= 8u) __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (k >= 4u) __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// make [.., target) resident: issue what is missing (and what the ring can
+// take beyond it), then wait for the chunks below target only -- the ones
+// issued after them (two LDS-DMA ops per chunk, completed in issue order as
+// vmcnt counts them) stay in flight into the next round
 __device__ __attribute__((always_inline)) inline void ld_until(TbLoader& L, ChainShared& sh, uint32_t first,
                                                               uint32_t target, uint32_t j1, const TbPre& pre,
                                                               uint32_t lane) {
     const uint32_t need = ((target < j1 ? target : j1) + 127u) / 128u;
     for (;;) {
         ld_issue(L, sh, first, j1, pre, lane);
+        if (L.next >= need) {
+            const uint32_t extra = L.next - need;      // chunks issued after the last needed one
+            ld_wait_at_most(2u * (extra < L.issued ? extra : L.issued));
+            L.issued = extra < L.issued ? extra : L.issued;
+            break;
+        }
         __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
         L.issued = 0;
-        if (L.next >= need) break;
     }
 }
 

@@ -1,9 +1,9 @@
 #!/bin/bash
 # branch-free producers vs the base build; GPU suite on the new build
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/span_tests.log 2>&1
-rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/span_tests.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/loader_tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 gpurun_out/loader_tests.log
 [ $rc -ge 124 ] && exit $rc
 BARGS="--lat-batches 0" STEPS=16 bash scripts/ab.sh librl_amd_base.so librl_amd.so librl_amd_base.so librl_amd.so || exit $?
 BARGS="--workload tb_zipf15 --lat-batches 0" STEPS=6 bash scripts/ab.sh librl_amd_base.so librl_amd.so || exit $?
-RL_AMD_LIB=$PWD/distributed-rate-limiter_amd/lib/librl_amd_stamps.so TAG=stamps_span bash scripts/bench_brief.sh
+RL_AMD_LIB=$PWD/distributed-rate-limiter_amd/lib/librl_amd_stamps.so TAG=stamps_loader bash scripts/bench_brief.sh
