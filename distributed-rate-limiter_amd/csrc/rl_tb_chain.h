@@ -804,11 +804,36 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
         if (same) {
             D = v.Dact;                     // same decade / binade (sign may flip)
         } else {
-            const TbQ nq = tb_quant(v.tokens, profile);
-            D = nq.D;
-            E = nq.E;
-            emode = fast_mode(D < 0 ? -D : D, E, profile);
-            if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
+            // a step out of a fast decade nearly always lands in a neighbouring
+            // one: its 14 digits there from one exact scaled rounding (valid in
+            // exactly one decade: the exact product >= 1e13 and the rounded
+            // digits < 1e14), else the general %.14g decomposition
+            bool nb = false;
+            if (emode == QM_DEC) {
+                const double at = v.tokens < 0.0 ? -v.tokens : v.tokens;
+#pragma unroll
+                for (int d = -1; d <= 1; d += 2) {
+                    const int32_t k2 = 13 - (E + d);
+                    if (nb || k2 < 1 || k2 > 22) continue;
+                    const double P2 = d < 0 ? Ps * 10.0 : Ps / 10.0;     // exact powers of ten (k2 <= 22)
+                    bool ge_lo;
+                    const double Dn = round_scaled_Pd(at, P2, ge_lo);
+                    if (at > 0.0 && ge_lo && Dn < (double)DEC_HI) {
+                        D = v.tokens < 0.0 ? -(int64_t)Dn : (int64_t)Dn;
+                        E = E + d;
+                        Ps = P2;
+                        Rs = RL_STEP_DIV ? 0.0 : 1.0 / P2;
+                        nb = true;
+                    }
+                }
+            }
+            if (!nb) {
+                const TbQ nq = tb_quant(v.tokens, profile);
+                D = nq.D;
+                E = nq.E;
+                emode = fast_mode(D < 0 ? -D : D, E, profile);
+                if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
+            }
         }
         const bool was_fast = mode != QM_NONE;
         mode = fast_mode(D, E, profile);
