@@ -12,6 +12,7 @@
 // Reference boundary replaced: go-redis Eval + Redis Lua + the Go arithmetic
 // around it (tokenbucket.go:90-193, slidingwindow.go:68-185,
 // fixedwindow.go:65-163); see include/rl_engine.h.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -494,6 +495,7 @@ struct rl_engine {
     bool timing = false;
     bool timing_all = false;    // level 2: every stage; level 1: the replay only (2 events per batch)
     bool stamps = false;        // RL_STAMP_KERNELS: timestamps around each replay (debug words 18, 19)
+    bool bind_events = true;    // replay timing events bound to the dispatch (RL_EV_MARKERS: marker packets)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::array<hipEvent_t, 8>> ev_pending;
     double stage_ms[NSTAGES] = {0, 0, 0, 0, 0};
@@ -711,6 +713,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
         if (hipMemset(e->stamp_ring, 0, 4 * 6 * STAMP_RING) != hipSuccess) return bail(RL_EDEVICE);
     }
     e->scatter_unpermute = getenv("RL_SCATTER_UNPERMUTE") != nullptr;
+    e->bind_events = getenv("RL_EV_MARKERS") == nullptr;
     if (const char* v = getenv("RL_PROBE_R")) e->probe_r = atoi(v) == 1 ? 1 : 4;
     {
         int dev_lds = 0;
@@ -905,37 +908,52 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // the TB reset time is state-independent: k_permute writes it straight
     // into the sorted result buffer
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
-    k_permute<<<pgrid_r, 256, GROUP_LDS, f>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, e->profile, B.rec, ps, pre);
+    // front_done rides on k_permute's dispatch packet (no marker packet)
+    // unless a stamp kernel follows it
+    const bool bind_front = e->bind_events && !sr;
+    hipExtLaunchKernelGGL(k_permute, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
+                          bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base, e->d_cfg,
+                          e->profile, B.rec, ps, pre);
     if (tall) (void)hipEventRecord(ev[3], f);
     if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 1);
-    HIPCHK(e, hipEventRecord(B.front_done, f));
+    if (!bind_front) HIPCHK(e, hipEventRecord(B.front_done, f));
 
     // replay: after this batch's grouping and the previous replay (stream
     // order on `chain`: the table state)
     hipStream_t c = e->chain, t = e->tail;
     HIPCHK(e, hipStreamWaitEvent(c, B.front_done, 0));
-    if (e->timing) (void)hipEventRecord(ev[4], c);
+    // replay timing: the two events ride on the replay's own dispatch packet
+    // (hipExtLaunchKernel) instead of two marker packets around it, unless
+    // the stamp kernels must sit inside the timed interval
+    const bool bound_ev = e->timing && !e->stamps && !sr && e->bind_events;
+    if (e->timing && !bound_ev) (void)hipEventRecord(ev[4], c);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 18);
     if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 2);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
+    // timing off: chain_done rides on the dispatch instead
+    const bool bind_done = !e->timing && !e->stamps && !sr && e->bind_events;
+    const hipEvent_t ev_a = bound_ev ? ev[4] : nullptr, ev_b = bound_ev ? ev[5] : bind_done ? B.chain_done : nullptr;
     if (ncfg <= (uint32_t)MAX_LCFG)
-        k_tb_chain<true><<<e->coop_grid, CH_BLOCK, e->chain_pad[0], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(),
-                                                           e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
-                                                           B.runs);
+        hipExtLaunchKernelGGL(k_tb_chain<true>, dim3(e->coop_grid), dim3(CH_BLOCK), (uint32_t)e->chain_pad[0], c, ev_a, ev_b,
+                              0u, kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(), e->d_cfg, ncfg,
+                              e->profile, ps, pre, e->d_eflags, dbg, B.runs);
     else
-        k_tb_chain<false><<<e->coop_grid, CH_BLOCK, e->chain_pad[1], c>>>(kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(),
-                                                            e->d_cfg, ncfg, e->profile, ps, pre, e->d_eflags, dbg,
-                                                            B.runs);
+        hipExtLaunchKernelGGL(k_tb_chain<false>, dim3(e->coop_grid), dim3(CH_BLOCK), (uint32_t)e->chain_pad[1], c, ev_a, ev_b,
+                              0u, kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(), e->d_cfg, ncfg,
+                              e->profile, ps, pre, e->d_eflags, dbg, B.runs);
+    HIPCHK(e, hipGetLastError());
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 19);
     if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 3);
     // the replay's end: with timing on, its timing event also orders the
-    // finish stream (one marker packet on the chain stream instead of two)
+    // finish stream (no extra marker packet on the chain stream)
     hipEvent_t chain_end = B.chain_done;
-    if (e->timing) {
+    if (bound_ev) {
+        chain_end = ev[5];
+    } else if (e->timing) {
         HIPCHK(e, hipEventRecord(ev[5], c));
         chain_end = ev[5];
-    } else {
+    } else if (!bind_done) {
         HIPCHK(e, hipEventRecord(B.chain_done, c));
     }
     // finish: outputs of the committed runs, results to the caller's order

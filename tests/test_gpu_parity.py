@@ -402,6 +402,47 @@ def test_device_api_batches_in_flight(rl, pipeline):
         assert_same(res, ref, configs, cfg, what=f"batch {i}")
 
 
+@pytest.mark.parametrize("level", [1, 2])
+def test_timed_pipelined_batches(rl, level):
+    """Stage timing on (level 1: the replay's events are bound to its dispatch
+    and also order the finish stream; level 2: marker events around every
+    stage) over pipelined hot-key batches: results equal the oracle's and the
+    replay time is reported."""
+    import torch
+    g = traces.TokenBucketZipf(batch=100_000)
+    eng = rl.Engine(profile=0, tb_capacity=1 << 20, win_capacity=1024, max_batch=1 << 17, flags=rl.OPT_PIPELINE)
+    sim = oracle.OracleSim(0)
+    for a, L, W in g.configs:
+        eng.register(a, L, W)
+        sim.add_config(a, L, W)
+    eng.set_timing(level)
+    eng.stage_times()
+    dev = torch.device("cuda", 0)
+    parts = [g.next_batch() for _ in range(4)]
+    ins, outs = [], []
+    for key, ts, n, cfg in parts:
+        ins.append([torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+                    for x in (key, ts, n, cfg.view(np.int32))])
+        m = key.size
+        outs.append([torch.empty(m, dtype=torch.uint8, device=dev)] +
+                    [torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)] +
+                    [torch.empty(m, dtype=torch.float64, device=dev)])
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for (k, t, n, c), o in zip(ins, outs):
+        eng.decide_device(k.numel(), k.data_ptr(), t.data_ptr(), n.data_ptr(), c.data_ptr(), None,
+                          *[x.data_ptr() for x in o], stream)
+    torch.cuda.synchronize()
+    assert eng.sync() == 0, eng.last_error()
+    ms, nb = eng.stage_times()
+    eng.set_timing(0)
+    assert nb == len(parts) and ms[3] > 0
+    for i, ((key, ts, n, cfg), o) in enumerate(zip(parts, outs)):
+        ref = sim.decide(key, ts, n, cfg)
+        res = rl.Decisions(*[x.cpu().numpy() for x in o])
+        assert_same(res, ref, g.configs, cfg, what=f"batch {i}")
+
+
 # --- table GC / resize (rl_table_gc) ----------------------------------------------
 
 @pytest.mark.parametrize("profile", [0, 1])
