@@ -131,6 +131,22 @@ struct ChState {
     uint32_t hot;       // diagnostics: segment of >= 65536 requests
 };
 
+// Speculative restart (RL_CH_SPEC): in a round whose chain window will
+// likely leave the regime, the producers predict the exit from nominal states
+// (the exit step q and the decade E of its result) and summarize the window
+// from q + 1 at scale 10^(13 - E) instead of the window after the chain's.
+// When the chain's exact exit and serial steps end at q + 1 in decade E, the
+// next round resolves that window at once -- no producers-only round.
+#ifndef RL_CH_SPEC
+#define RL_CH_SPEC 1
+#endif
+struct ChSpec {
+    uint32_t valid;
+    uint32_t first, cnt;   // window [first, first + cnt), summarized in tile[buf]
+    uint32_t buf;
+    int32_t E;             // decimal mode at 10^(13 - E)
+};
+
 struct ChainShared {
     double2 r_add[RING_G];       // TbPre::add
     double2 r_th[RING_G];        // TbPre::th
@@ -141,6 +157,7 @@ struct ChainShared {
     uint16_t ne_rank[2][CH_NP][64];    // near steps of the tile before each producer lane
     int32_t ne_off[CH_NP * CH_NE];     // chain: resolved offset after each near step
     ChState st[2];
+    ChSpec spec[2];                    // producers' speculative window of the round (RL_CH_SPEC)
 };
 
 __device__ inline double ring_add(const ChainShared& sh, uint32_t p) {
@@ -545,6 +562,80 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
         T.ev = ev_t;
         T.nc = ninc;
     }
+}
+
+// The chain window's likely regime exit (decimal mode; every producer wave
+// computes the same): the first tile whose bounds admit an exit at the
+// nominal state, its steps replayed from nominal lane starts; the exit step's
+// result (sum - th when it allows, else sum) decides the decade E.  A guess:
+// the chain adopts the window only if its exact replay agrees (ch_segment).
+__device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainShared& sh, const ChState& s, double P,
+                                                                  double R, uint32_t j1) {
+    constexpr int K = CH_K;
+    ChSpec sp{0u, 0u, 0u, 0u, 0};
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nt = (s.ccnt + CH_TILE - 1) / CH_TILE;
+    const bool tv = lane < nt;
+    const ChTile T = sh.tile[s.cbuf][tv ? lane : 0u];
+    const int64_t Sl = tv ? T.S : 0;
+    const int64_t Dt = s.D + wave_incl_scan_i64(Sl) - Sl;          // nominal start of tile t
+    const double dD = (double)Dt;
+    const bool cand = tv && (T.ev != NO_STOP || !(dD + T.cmax < (double)DEC_HI) ||
+                             !(dD + T.cmin >= (double)DEC_LO + 1.0) || !(dD + 3.0 < T.ymin));
+    const uint64_t cm = __ballot(cand);
+    if (!cm) return sp;
+    const uint32_t c = first_lane(cm);
+    const int64_t Dc = readlane_i64(Dt, c);
+    const uint32_t p0 = s.cfirst + c * CH_TILE;
+    const uint32_t clen = (s.ccnt - c * CH_TILE) < CH_TILE ? (s.ccnt - c * CH_TILE) : CH_TILE;
+    const uint32_t off = lane * K;
+    const uint32_t nv = off < clen ? ((clen - off) < (uint32_t)K ? (clen - off) : (uint32_t)K) : 0u;
+    double add[K], th[K];
+    int64_t S = 0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const bool v = (uint32_t)q < nv;
+        add[q] = v ? ring_add(sh, p0 + off + q) : 0.0;
+        th[q] = v ? ring_th(sh, p0 + off + q) : __builtin_inf();
+        const double pr = add[q] * P;
+        if (fabs(pr) < 0x1p49) S += (int64_t)rint(pr);
+    }
+    const int64_t incl = wave_incl_scan_i64(S);
+    double D = (double)(Dc + incl - S);
+    uint32_t bq = NO_STOP;
+    double sum_b = 0.0, th_b = 0.0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const bool act = (uint32_t)q < nv && bq == NO_STOP;
+        double tk;
+        const double Dn = tb_step_d<QM_DEC>(D, P, R, add[q], th[q], tk);
+        const bool stop = act && !(Dn == Dn);
+        bq = stop ? (uint32_t)q : bq;
+        sum_b = stop ? tk : sum_b;
+        th_b = stop ? th[q] : th_b;
+        D = (act && !stop) ? Dn : D;
+    }
+    const uint32_t fb = first_lane(__ballot(bq != NO_STOP));
+    if (fb >= 64u) return sp;
+    const uint32_t first = p0 + fb * K + (uint32_t)__builtin_amdgcn_readlane((int)bq, (int)fb) + 1u;
+    const double sum = readlane_f64(sum_b, fb), thv = readlane_f64(th_b, fb);
+    const double post = sum >= thv ? sum - thv : sum;
+    if (first >= j1 || !(post > 0.0) || !(post < 1e12)) return sp;
+    const int e0 = (int)floor(log10(post));
+#pragma unroll
+    for (int d = -1; d <= 1; d++) {
+        const int e = e0 + d, k = 13 - e;
+        if (sp.valid || k < 1 || k > 22) continue;
+        bool ge_lo;
+        const double Dn = round_scaled_Pd(post, rlq::pow10_exact(k), ge_lo);
+        if (ge_lo && Dn < (double)DEC_HI) {
+            sp.valid = 1u;
+            sp.E = e;
+        }
+    }
+    sp.first = first;
+    sp.cnt = (j1 - first) < CH_W ? (j1 - first) : CH_W;
+    return sp;
 }
 
 // ---------------------------------------------------------------------------
@@ -1085,6 +1176,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         s0.cbuf = 1;
         s0.hot = j1 - j0 >= 65536u;
         sh.st[0] = s0;
+        sh.spec[0].valid = 0u;
     }
     if (wave == (uint32_t)CH_LOADER) {
         ld_until(L, sh, j0, j0 + 2 * CH_W, j1, pre, lane);
@@ -1098,7 +1190,30 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     }
     lds_barrier();
     for (;;) {
-        const ChState s = sh.st[par];
+        ChState s = sh.st[par];
+        if (RL_CH_SPEC) {
+            const ChSpec sp = sh.spec[par];
+            if (sp.valid) {
+                if (s.ccnt == 0 && s.mode == QM_DEC && s.pfirst == sp.first && s.E == sp.E) {
+                    // the chain's exit ended where the producers guessed: their
+                    // window is the next chain window
+                    s.cfirst = sp.first;
+                    s.ccnt = sp.cnt;
+                    s.cbuf = sp.buf;
+                    s.pbuf = sp.buf ^ 1u;
+                    s.pfirst = sp.first + sp.cnt;
+                    if (dbg && threadIdx.x == 0) atomicAdd(&dbg[22], 1u);
+                } else {
+                    // the chain went elsewhere: tile[s.cbuf] does not hold its
+                    // next window (the state is exact at s.cfirst / s.pfirst)
+                    if (s.ccnt > 0) {
+                        s.pfirst = s.cfirst;
+                        s.ccnt = 0;
+                    }
+                    if (dbg && threadIdx.x == 0) atomicAdd(&dbg[23], 1u);
+                }
+            }
+        }
         if (s.ccnt == 0 && s.pfirst >= j1) break;                 // block-uniform
         const uint32_t pcnt = (s.mode != QM_NONE && s.pfirst < j1) ? ((j1 - s.pfirst) < CH_W ? (j1 - s.pfirst) : CH_W)
                                                                    : 0u;
@@ -1107,7 +1222,17 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         nrounds++;
         CH_T(t0);
         if (ch_producer_index(wave) >= 0) {
-            if (pcnt) {
+            ChSpec sp{0u, 0u, 0u, 0u, 0};
+            if (RL_CH_SPEC && s.ccnt > 0 && s.mode == QM_DEC) sp = ch_predict(sh, s, P, R, j1);
+            if (RL_CH_SPEC && ch_producer_index(wave) == 0 && (threadIdx.x & 63) == 0) {
+                sp.buf = s.pbuf;
+                sh.spec[par ^ 1u] = sp;
+            }
+            if (sp.valid) {
+                double P2, R2;
+                mode_scale(QM_DEC, sp.E, P2, R2);
+                ch_produce<QM_DEC>(sh, s.pbuf, ch_producer_index(wave), sp.first, sp.cnt, P2, (double)DEC_HI);
+            } else if (pcnt) {
                 if (s.mode == QM_DEC) {
                     // bound on the window's states: the chain window's base plus
                     // 2.25x its nominal growth (the chain verifies it per tile)
