@@ -407,6 +407,10 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
                           "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
+                          # speculative restart windows: adopted, rejected (the chain's exit
+                          # ended 1 / 2-64 / > 64 steps after the guess, other)
+                          "spec_windows": [int(dbgw[22]), int(dbgw[23]), int(dbgw[9]), int(dbgw[10]),
+                                           int(dbgw[11]), int(dbgw[15])],
                           "replay_timeline_us": {"hot_start": ((int(dbgw[16]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
                                                  "hot_end": ((int(dbgw[17]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
                                                  "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,

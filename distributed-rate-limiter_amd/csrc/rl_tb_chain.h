@@ -567,8 +567,10 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
 // The chain window's likely regime exit (decimal mode; every producer wave
 // computes the same): the first tile whose bounds admit an exit at the
 // nominal state, its steps replayed from nominal lane starts; the exit step's
-// result (sum - th when it allows, else sum) decides the decade E.  A guess:
-// the chain adopts the window only if its exact replay agrees (ch_segment).
+// result (sum - th when it allows, else sum), carried on through the serial
+// steps that follow an allow or a balance <= 0, decides the decade E.  A
+// guess: the chain adopts the window only if its exact replay agrees
+// (ch_segment).
 __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainShared& sh, const ChState& s, double P,
                                                                   double R, uint32_t j1) {
     constexpr int K = CH_K;
@@ -617,10 +619,36 @@ __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainSh
     }
     const uint32_t fb = first_lane(__ballot(bq != NO_STOP));
     if (fb >= 64u) return sp;
-    const uint32_t first = p0 + fb * K + (uint32_t)__builtin_amdgcn_readlane((int)bq, (int)fb) + 1u;
+    uint32_t first = p0 + fb * K + (uint32_t)__builtin_amdgcn_readlane((int)bq, (int)fb) + 1u;
     const double sum = readlane_f64(sum_b, fb), thv = readlane_f64(th_b, fb);
-    const double post = sum >= thv ? sum - thv : sum;
-    if (first >= j1 || !(post > 0.0) || !(post < 1e12)) return sp;
+    const bool allow = sum >= thv;
+    double post = allow ? sum - thv : sum;
+    if (first >= j1 || !(post == post)) return sp;
+    if (allow || !(post > 0.0)) {
+        // the serial steps go on after an allow (the next step too) and while
+        // the balance is at or below zero (off the fast decades): they end
+        // after the first step that leaves it positive -- the first positive
+        // partial sum of the next adds, if no step on the way allows or
+        // expires and the serial steps of one round reach it
+        const uint32_t p = first + lane;
+        const bool ok = p < j1 && lane < (uint32_t)CH_SERIAL - 1u;
+        const double ad = ok ? ring_add(sh, p) : 0.0;
+        const double tv2 = ok ? ring_th(sh, p) : __builtin_inf();
+        double c = ad;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const double u = __shfl_up(c, o, 64);
+            c = lane >= (uint32_t)o ? c + u : c;
+        }
+        const double vsum = post + c;
+        const uint32_t fp = first_lane(__ballot(ok && vsum > 0.0));
+        const uint32_t fx = first_lane(__ballot(ok && (vsum >= tv2 || !(ad == ad))));
+        if (fp >= 64u || fx <= fp) return sp;
+        post = readlane_f64(vsum, fp);
+        first += fp + 1u;
+        if (first >= j1) return sp;
+    }
+    if (!(post < 1e12)) return sp;
     const int e0 = (int)floor(log10(post));
 #pragma unroll
     for (int d = -1; d <= 1; d++) {
@@ -1210,7 +1238,13 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                         s.pfirst = s.cfirst;
                         s.ccnt = 0;
                     }
-                    if (dbg && threadIdx.x == 0) atomicAdd(&dbg[23], 1u);
+                    if (dbg && threadIdx.x == 0) {
+                        atomicAdd(&dbg[23], 1u);
+                        // why: [9] the chain went on, [10] / [11] it ended after /
+                        // before the guess, [15] another decade or mode
+                        const uint32_t dd = s.pfirst - sp.first;
+                        atomicAdd(&dbg[s.ccnt > 0 || s.pfirst <= sp.first ? 15 : dd == 1u ? 9 : dd <= 64u ? 10 : 11], 1u);
+                    }
                 }
             }
         }
