@@ -408,9 +408,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
                           # speculative restart windows: adopted, rejected (the chain's exit
-                          # ended 1 / 2-64 / > 64 steps after the guess, other)
+                          # ended 1 / 2-64 steps after the guess, other)
                           "spec_windows": [int(dbgw[22]), int(dbgw[23]), int(dbgw[9]), int(dbgw[10]),
-                                           int(dbgw[11]), int(dbgw[15])],
+                                           int(dbgw[15])],
                           "replay_timeline_us": {"hot_start": ((int(dbgw[16]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
                                                  "hot_end": ((int(dbgw[17]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
                                                  "last_block_end": ((int(dbgw[14]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100,
@@ -418,7 +418,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                                                  "stamp_before": (((int(dbgw[18]) - (~int(dbgw[13]) & 0xffffffff) + (1 << 31)) & 0xffffffff) - (1 << 31)) / 100 if dbgw[18] else None,
                                                  "stamp_after": (((int(dbgw[19]) - (~int(dbgw[13]) & 0xffffffff) + (1 << 31)) & 0xffffffff) - (1 << 31)) / 100 if dbgw[19] else None},
                           "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
-                          "near_setup_x16": int(dbgw[39]) * 16},
+                          "near_setup_x16": int(dbgw[39]) * 16,
+                          # stamps build: the hot chain's exact tiles (cycles, passes)
+                          "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])]},
         "latency": latency,
         "stamp_ring": stamp_ring,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],

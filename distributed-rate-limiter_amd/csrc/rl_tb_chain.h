@@ -566,7 +566,8 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
 
 // The chain window's likely regime exit (decimal mode; every producer wave
 // computes the same): the first tile whose bounds admit an exit at the
-// nominal state, its steps replayed from nominal lane starts; the exit step's
+// nominal state, the first nominal exit in it (nominal digit sums, no %.14g
+// steps); the exit step's
 // result (sum - th when it allows, else sum), carried on through the serial
 // steps that follow an allow or a balance <= 0, decides the decade E.  A
 // guess: the chain adopts the window only if its exact replay agrees
@@ -603,24 +604,28 @@ __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainSh
         if (fabs(pr) < 0x1p49) S += (int64_t)rint(pr);
     }
     const int64_t incl = wave_incl_scan_i64(S);
+    // nominal states (integer digits, no %.14g step): an exit where the sum
+    // reaches th (D + add P >= th P) or the next digits leave the decade
     double D = (double)(Dc + incl - S);
     uint32_t bq = NO_STOP;
-    double sum_b = 0.0, th_b = 0.0;
+    double D_b = 0.0, a_b = 0.0, th_b = 0.0;
 #pragma unroll
     for (int q = 0; q < K; q++) {
-        const bool act = (uint32_t)q < nv && bq == NO_STOP;
-        double tk;
-        const double Dn = tb_step_d<QM_DEC>(D, P, R, add[q], th[q], tk);
-        const bool stop = act && !(Dn == Dn);
+        const double pr = add[q] * P;
+        const double Dn = D + rint(pr);
+        const bool stop = (uint32_t)q < nv && bq == NO_STOP &&
+                          (!(fabs(pr) < 0x1p49) || !(D + pr < th[q] * P) || !(Dn < (double)DEC_HI) ||
+                           !(Dn >= (double)DEC_LO));
         bq = stop ? (uint32_t)q : bq;
-        sum_b = stop ? tk : sum_b;
+        D_b = stop ? D : D_b;
+        a_b = stop ? add[q] : a_b;
         th_b = stop ? th[q] : th_b;
-        D = (act && !stop) ? Dn : D;
+        D = Dn;
     }
     const uint32_t fb = first_lane(__ballot(bq != NO_STOP));
     if (fb >= 64u) return sp;
     uint32_t first = p0 + fb * K + (uint32_t)__builtin_amdgcn_readlane((int)bq, (int)fb) + 1u;
-    const double sum = readlane_f64(sum_b, fb), thv = readlane_f64(th_b, fb);
+    const double sum = readlane_f64(D_b, fb) / P + readlane_f64(a_b, fb), thv = readlane_f64(th_b, fb);
     const bool allow = sum >= thv;
     double post = allow ? sum - thv : sum;
     if (first >= j1 || !(post == post)) return sp;
@@ -831,7 +836,17 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 goff = (gi > cn0 && gc) ? sh.ne_off[gc - 1] - cin : 0;
             }
             int64_t Dq = 0;
+#ifdef RL_STAMPS
+            const uint64_t t_ex = __builtin_amdgcn_s_memtime();
+            const uint32_t it_ex = iters;
+#endif
             uint32_t brk = exact_span<MODE, false>(RingSrc{sh}, cpos, clen, Dc, goff, P, R, Dq, a, iters);
+#ifdef RL_STAMPS
+            if (dbg && lane == 0 && s.hot) {   // [7] cycles / 16, [11] passes of the hot chain's exact tiles
+                atomicAdd(&dbg[7], (uint32_t)((__builtin_amdgcn_s_memtime() - t_ex) >> 4));
+                atomicAdd(&dbg[11], iters - it_ex);
+            }
+#endif
             if (brk > clen) {       // (never) give up on the window: one exact serial step
                 if (lane == 0) atomicOr(eflags, EF_INTERNAL);
                 brk = 0;
@@ -1240,10 +1255,10 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                     }
                     if (dbg && threadIdx.x == 0) {
                         atomicAdd(&dbg[23], 1u);
-                        // why: [9] the chain went on, [10] / [11] it ended after /
-                        // before the guess, [15] another decade or mode
+                        // why: the chain's exit ended [9] 1 or [10] 2-64 steps after
+                        // the guess, [15] anything else
                         const uint32_t dd = s.pfirst - sp.first;
-                        atomicAdd(&dbg[s.ccnt > 0 || s.pfirst <= sp.first ? 15 : dd == 1u ? 9 : dd <= 64u ? 10 : 11], 1u);
+                        atomicAdd(&dbg[s.ccnt > 0 || s.pfirst <= sp.first || dd > 64u ? 15 : dd == 1u ? 9 : 10], 1u);
                     }
                 }
             }
@@ -1258,6 +1273,11 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         if (ch_producer_index(wave) >= 0) {
             ChSpec sp{0u, 0u, 0u, 0u, 0};
             if (RL_CH_SPEC && s.ccnt > 0 && s.mode == QM_DEC) sp = ch_predict(sh, s, P, R, j1);
+#ifdef RL_STAMPS
+            CH_T(t1);
+            cyc[1] += t1 - t0;          // producers: the exit guess
+            cyc[2] += sp.valid;         // producers: windows guessed
+#endif
             if (RL_CH_SPEC && ch_producer_index(wave) == 0 && (threadIdx.x & 63) == 0) {
                 sp.buf = s.pbuf;
                 sh.spec[par ^ 1u] = sp;

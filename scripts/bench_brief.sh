@@ -13,5 +13,5 @@ print(sys.argv[1], "| %.1f M/s" % (d["value"] / 1e6),
       "ends", r.get("round_ends_full_stop_partial_first"), "exact", r.get("exact_tiles"), "serial", r.get("serial_steps"), "timeline", r.get("replay_timeline_us"))
 st = r.get("stamps_x16")
 if st and any(st):
-    print("  chain [full, stop, serial, barrier]", st[0:4], " producer [work,-,-,barrier]", st[4:8], " loader", st[8:12], " hot: near cyc/entries/iters", st[12], [int(x) for x in r.get("near_hot", [])], "setup", r.get("near_setup_x16"), " hw_id", r.get("hw_id"))
+    print("  chain [full, stop, serial, barrier]", st[0:4], " producer [work,-,-,barrier]", st[4:8], " loader", st[8:12], " hot: near cyc/entries/iters", st[12], [int(x) for x in r.get("near_hot", [])], "setup", r.get("near_setup_x16"), "exact", r.get("exact_hot_x16"), " hw_id", r.get("hw_id"))
 PY
