@@ -464,6 +464,7 @@ struct rl_engine {
     uint8_t* s_dec = nullptr;
     double *s_tok = nullptr, *s_add = nullptr, *s_lq = nullptr, *s_th = nullptr;
     hipEvent_t ev_small = nullptr;
+    hipEvent_t ev_reset = nullptr;    // rl_reset_device: the DEL on `chain` -> the caller's stream
     int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
     size_t zero_bytes = 0;
     int coop_grid = 96;         // k_tb_chain blocks (one per CU fits its LDS): 96 of 256 CUs, the
@@ -515,6 +516,17 @@ static int fail(rl_engine* e, int code, const std::string& msg) {
         if (_st != hipSuccess)                                                           \
             return fail((e), RL_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_st)); \
     } while (0)
+
+// versioned output structs (include/rl_engine.h): the caller's struct_size
+// bounds what is written; a size smaller than the header field is rejected
+template <class T>
+static int copy_out(T* dst, T src) {
+    if (dst->struct_size < 8) return RL_EINVAL;
+    const uint32_t n = dst->struct_size;
+    src.struct_size = n;
+    memcpy(dst, &src, std::min<size_t>(n, sizeof(T)));
+    return RL_OK;
+}
 
 static void free_set(BatchSet& B) {
     (void)hipFree(B.sk0); (void)hipFree(B.sk1); (void)hipFree(B.sv0); (void)hipFree(B.sv1);
@@ -594,6 +606,7 @@ static void free_all(rl_engine* e) {
     for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
     if (e->ev_in) (void)hipEventDestroy(e->ev_in);
     if (e->ev_small) (void)hipEventDestroy(e->ev_small);
+    if (e->ev_reset) (void)hipEventDestroy(e->ev_reset);
     for (void* p : {(void*)e->s_ts, (void*)e->s_n, (void*)e->s_sms, (void*)e->s_rem, (void*)e->s_retry,
                     (void*)e->s_reset, (void*)e->s_when, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
                     (void*)e->s_add, (void*)e->s_lq, (void*)e->s_th})
@@ -620,6 +633,7 @@ static int warm_up(rl_engine* e);
 extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (!o || !out) return RL_EINVAL;
     *out = nullptr;
+    if (o->struct_size != sizeof(rl_opts)) return RL_EINVAL;
     if (o->profile != PROFILE_REDIS7 && o->profile != PROFILE_MINIREDIS) return RL_EINVAL;
     if (o->max_batch == 0 || o->max_batch > (1u << 28)) return RL_EINVAL;
     if (o->flags & ~(uint32_t)RL_OPT_PIPELINE) return RL_EINVAL;
@@ -666,6 +680,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     e->stream = e->tail;
     if (hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
     if (hipEventCreateWithFlags(&e->ev_small, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
+    if (hipEventCreateWithFlags(&e->ev_reset, hipEventDisableTiming) != hipSuccess) return bail(RL_EDEVICE);
     e->small_max = SMALL_MAX;
     if (const char* v = getenv("RL_SMALL_MAX")) e->small_max = std::min<uint32_t>((uint32_t)atoi(v), SMALL_MAX);
     size_t M = e->max_batch;
@@ -1104,20 +1119,31 @@ extern "C" int rl_decide_batch(rl_engine* e, size_t m, const uint64_t* key_id, c
     return check_flags(e, f);
 }
 
-extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns) {
+// The DEL only writes `when` fields of table entries, which only the replays
+// (k_tb_chain, k_small: both on `chain`) read; the grouping reads entry keys
+// only and the finish no table state.  So one kernel on `chain` between two
+// replays is exactly "after every earlier batch, before every later one".
+extern "C" int rl_reset_device(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns, void* stream) {
     if (!e || cfg_id >= e->h_cfg.size() || key_id == EMPTY_KEY) return RL_EINVAL;
     (void)hipSetDevice(e->device);
-    int r = drain(e);
-    if (r != RL_OK) return r;
-    k_reset<<<1, 1, 0, e->stream>>>(key_id, ts_ns, e->d_cfg, cfg_id, e->d_tb, e->tb_cap - 1, e->d_win,
-                                     e->win_cap - 1, e->spill());
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    k_reset<<<1, 1, 0, e->chain>>>(key_id, ts_ns, e->d_cfg, cfg_id, e->d_tb, e->tb_cap - 1, e->d_win,
+                                    e->win_cap - 1, e->spill());
     HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->ev_reset, e->chain));
+    HIPCHK(e, hipStreamWaitEvent(s, e->ev_reset, 0));
+    return RL_OK;
+}
+
+extern "C" int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns) {
+    const int r = rl_reset_device(e, cfg_id, key_id, ts_ns, nullptr);
+    if (r != RL_OK) return r;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return RL_OK;
 }
 
 extern "C" int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* out) {
-    if (!e || !out) return RL_EINVAL;
+    if (!e || !out || out->struct_size < 8) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     int r = drain(e);
     if (r != RL_OK) return r;
@@ -1133,13 +1159,13 @@ extern "C" int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* ou
     ok = ok && hipStreamSynchronize(s) == hipSuccess;
     (void)hipFree(d);
     if (!ok) return fail(e, RL_EDEVICE, "table count failed");
-    *out = rl_table_info{e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3], e->spill_cap, h[4], h[5]};
-    return RL_OK;
+    return copy_out(out, rl_table_info{sizeof(rl_table_info), 0, e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3],
+                                       e->spill_cap, h[4], h[5]});
 }
 
 extern "C" int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, uint64_t win_capacity,
                            rl_table_info* out) {
-    if (!e) return RL_EINVAL;
+    if (!e || (out && out->struct_size < 8)) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     const uint64_t tb_cap = tb_capacity ? pow2_at_least(std::max<uint64_t>(tb_capacity, 1024)) : e->tb_cap;
     const uint64_t win_cap = win_capacity ? pow2_at_least(std::max<uint64_t>(win_capacity, 1024)) : e->win_cap;
@@ -1200,7 +1226,7 @@ extern "C" int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, u
 }
 
 extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
-    if (!e || !out) return RL_EINVAL;
+    if (!e || !out || out->struct_size < 8) return RL_EINVAL;
     (void)hipSetDevice(e->device);
     uint32_t c[4] = {0, 0, 0, 0}, d[24] = {0};
     int r = drain(e);
@@ -1220,8 +1246,7 @@ extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
     e->stats.last_coop_rounds = d[0];
     e->stats.last_coop_iters = d[1];
     for (int k = 0; k < 4; k++) e->stats.coop_ends[k] = d[3 + k];
-    *out = e->stats;
-    return RL_OK;
+    return copy_out(out, e->stats);
 }
 
 extern "C" int rl_engine_set_timing(rl_engine* e, int on) {

@@ -151,6 +151,7 @@ int main(int argc, char** argv) {
     }
 
     rl_opts o{};
+    o.struct_size = sizeof o;
     o.device = a.device;
     o.profile = RL_PROFILE_REDIS7;
     o.tb_capacity = 1 << 21;
@@ -162,6 +163,7 @@ int main(int argc, char** argv) {
     uint32_t cfg = 0;
     if (rl_config_register(e, RL_ALG_TOKEN_BUCKET, a.limit, (int64_t)(a.window_s * NS), &cfg) != RL_OK) return 1;
     rl_coalescer_opts co{};
+    co.struct_size = sizeof co;
     co.max_batch = a.max_batch;
     co.max_in_flight = 3;
     co.linger_ns = a.linger_ns;
@@ -174,7 +176,8 @@ int main(int argc, char** argv) {
     for (double qps : a.qps) {
         const int G = a.gens;
         const double rate = qps / G;   // per generator, per second
-        rl_coalescer_stats s0;
+        rl_coalescer_stats s0{};
+        s0.struct_size = sizeof s0;
         rl_coalescer_get_stats(c, &s0);
         std::vector<Hist> hist(G);
         // worst latency by arrival time, 100 ms buckets (where a tail comes from)
@@ -267,7 +270,8 @@ int main(int argc, char** argv) {
         Hist h;
         uint64_t tot = 0, drop = 0;
         for (int g = 0; g < G; g++) { h.merge(hist[g]); tot += sent[g]; drop += dropped[g]; }
-        rl_coalescer_stats s1;
+        rl_coalescer_stats s1{};
+        s1.struct_size = sizeof s1;
         rl_coalescer_get_stats(c, &s1);
         const double span = (double)(last_done.load() - start) / NS;
         const uint64_t nb = s1.batches - s0.batches;

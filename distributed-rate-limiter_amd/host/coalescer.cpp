@@ -26,8 +26,14 @@ void Sub::carve(size_t m_) {
     taken = 0;
     left = m_;
     status = RL_OK;
-    reset_op = done = waiting = false;
+    op = OP_REQ;
+    deadline = 0;
+    done = waiting = cancelled = dropped = in_queue = waited = false;
+    inflight = 0;
     done_ns = submit_ns = 0;
+    now_ms = 0;
+    cap_tb = cap_win = 0;
+    info = rl_table_info{};
     // layout by capacity, so a reused buffer keeps its arrays in place
     const size_t c = cap;
     uint8_t* p = mem.get();
@@ -123,13 +129,26 @@ public:
         ok &= hipEventRecord(d.ev, os_) == hipSuccess;
         return ok ? RL_OK : RL_EDEVICE;
     }
+    int launch_reset(int i, Slot& s, uint32_t cfg, uint64_t key, int64_t ts) override {
+        (void)hipSetDevice(dev_id_);   // the submitter thread
+        s.t_h2d = steady_ns();
+        // enqueued on the engine's replay stream between two batches; the
+        // output stream (and so this slot's completion event) waits for it
+        const int rc = rl_reset_device(e_, cfg, key, ts, os_);
+        if (rc != RL_OK) return rc;
+        return hipEventRecord(dev_[i].ev, os_) == hipSuccess ? RL_OK : RL_EDEVICE;
+    }
     int wait(int i, Slot&) override {
         (void)hipSetDevice(dev_id_);   // the completer thread
         return await_event(dev_[i].ev) == hipSuccess ? RL_OK : RL_EDEVICE;
     }
-    int reset(uint32_t cfg, uint64_t key, int64_t ts) override {
-        (void)hipSetDevice(dev_id_);   // the submitter thread
-        return rl_reset(e_, cfg, key, ts);
+    int table_info(int64_t now_ms, rl_table_info* out) override {
+        (void)hipSetDevice(dev_id_);
+        return rl_table_info_get(e_, now_ms, out);
+    }
+    int gc(int64_t now_ms, uint64_t tb_cap, uint64_t win_cap, rl_table_info* out) override {
+        (void)hipSetDevice(dev_id_);
+        return rl_table_gc(e_, now_ms, tb_cap, win_cap, out);
     }
 
 private:
@@ -158,10 +177,10 @@ private:
     size_t M_ = 0;
 };
 
-// synchronous host function (the CPU tests plug the oracle in here)
+// synchronous host functions (the CPU tests plug the oracle in here)
 class FnBackend : public Backend {
 public:
-    FnBackend(rl_batch_fn fn, rl_reset_fn rfn, void* user) : fn_(fn), rfn_(rfn), user_(user) {}
+    explicit FnBackend(const rl_coalescer_backend& b) : b_(b) {}
     int init(int nslots, size_t M, std::vector<Slot>* slots) override {
         slots->resize(nslots);
         mem_.resize(nslots);
@@ -182,26 +201,32 @@ public:
     }
     int launch(int, Slot& s) override {
         s.t_h2d = steady_ns();
-        return fn_(user_, s.m, s.key, s.ts, s.n, s.cfg, s.dec, s.rem, s.retry, s.reset);
+        return b_.batch(b_.user, s.m, s.key, s.ts, s.n, s.cfg, s.dec, s.rem, s.retry, s.reset);
+    }
+    int launch_reset(int, Slot& s, uint32_t cfg, uint64_t key, int64_t ts) override {
+        s.t_h2d = steady_ns();
+        return b_.reset ? b_.reset(b_.user, cfg, key, ts) : RL_EINVAL;
     }
     int wait(int, Slot&) override { return RL_OK; }
-    int reset(uint32_t cfg, uint64_t key, int64_t ts) override {
-        return rfn_ ? rfn_(user_, cfg, key, ts) : RL_EINVAL;
+    int table_info(int64_t now_ms, rl_table_info* out) override {
+        return b_.table_info ? b_.table_info(b_.user, now_ms, out) : RL_EINVAL;
+    }
+    int gc(int64_t now_ms, uint64_t tb_cap, uint64_t win_cap, rl_table_info* out) override {
+        return b_.gc ? b_.gc(b_.user, now_ms, tb_cap, win_cap, out) : RL_EINVAL;
     }
 
 private:
-    rl_batch_fn fn_;
-    rl_reset_fn rfn_;
-    void* user_;
+    rl_coalescer_backend b_;
     std::vector<std::unique_ptr<uint8_t[]>> mem_;
 };
 
 std::unique_ptr<Backend> make_gpu_backend(rl_engine* e) { return std::unique_ptr<Backend>(new GpuBackend(e)); }
-std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, rl_reset_fn rfn, void* user) {
-    return std::unique_ptr<Backend>(new FnBackend(fn, rfn, user));
+std::unique_ptr<Backend> make_fn_backend(const rl_coalescer_backend& b) {
+    return std::unique_ptr<Backend>(new FnBackend(b));
 }
 
 // ---------------------------------------------------------------------------
+
 
 Coalescer::Coalescer(std::unique_ptr<Backend> be, const rl_coalescer_opts& o) : be_(std::move(be)), o_(o) {
     if (o_.max_batch == 0) o_.max_batch = 65536;
@@ -209,7 +234,11 @@ Coalescer::Coalescer(std::unique_ptr<Backend> be, const rl_coalescer_opts& o) : 
     if (o_.max_in_flight > 3) o_.max_in_flight = 3;
     if (o_.queue_cap == 0) o_.queue_cap = 1ull << 24;
     if (o_.linger_ns < 0) o_.linger_ns = 0;
+    if (o_.gc_high_pct == 0 || o_.gc_high_pct > 95) o_.gc_high_pct = 50;
+    if (o_.gc_margin_ms <= 0) o_.gc_margin_ms = 1000;
+    if (o_.gc_interval_ns < 0) o_.gc_interval_ns = 0;
     if (const char* v = getenv("RL_COALESCER_TRACE")) trace_cap_ = (size_t)strtoull(v, nullptr, 10);
+    st_.struct_size = sizeof(rl_coalescer_stats);
 }
 
 int Coalescer::start() {
@@ -249,10 +278,10 @@ void Coalescer::Shutdown() {
 }
 
 int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
-                      uint64_t* ticket, bool reset_op) {
-    if (!ticket || (m && (!key || !ts || !n || !cfg)) || (reset_op && m != 1)) return RL_EINVAL;
+                      uint64_t* ticket, int64_t deadline) {
+    if (!ticket || (m && (!key || !ts || !n || !cfg)) || deadline < 0) return RL_EINVAL;
     Sub* s = get_sub(m);
-    s->reset_op = reset_op;
+    s->deadline = deadline;
     if (trace_cap_) s->submit_ns = steady_ns();
     memcpy(s->key, key, 8 * m);
     memcpy(s->ts, ts, 8 * m);
@@ -272,6 +301,7 @@ int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const in
         st_.submitted += m;
         if (m) {
             queue_.push_back(s);
+            s->in_queue = true;
             pending_ += m;
         } else {
             s->done = true;
@@ -286,28 +316,112 @@ int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const in
     return RL_OK;
 }
 
+int Coalescer::SubmitOp(Op op, uint64_t key, int64_t ts, uint32_t cfg, int64_t now_ms, uint64_t cap_tb,
+                        uint64_t cap_win, uint64_t* ticket) {
+    Sub* s = get_sub(1);
+    s->op = op;
+    s->key[0] = key;
+    s->ts[0] = ts;
+    s->n[0] = 1;
+    s->cfg[0] = cfg;
+    s->now_ms = now_ms;
+    s->cap_tb = cap_tb;
+    s->cap_win = cap_win;
+    if (trace_cap_) s->submit_ns = steady_ns();
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (stop_) {
+            put_sub(s);
+            return RL_ECLOSED;
+        }
+        s->first = next_seq_++;
+        subs_[s->first] = s;
+        queue_.push_back(s);
+        s->in_queue = true;
+        pending_ += 1;
+        *ticket = s->first;
+        if (!sub_idle_) return RL_OK;
+    }
+    cv_sub_.notify_one();
+    return RL_OK;
+}
+
+void Coalescer::drop_locked(Sub* s, int code) {
+    // none of it was launched: every request is still pending
+    pending_ -= s->m - s->taken;
+    if (s->op == OP_REQ) (code == RL_ECANCELED ? st_.cancelled : st_.expired) += s->m;
+    s->dropped = true;
+    s->done = true;
+    s->status = code;
+    s->left = 0;
+    s->done_ns = steady_ns();
+    if (s->waiting) s->cv.notify_all();
+}
+
+void Coalescer::maybe_free_locked(Sub* s) {
+    if (s->waited && !s->in_queue && s->inflight == 0) put_sub(s);
+}
+
+int Coalescer::Cancel(uint64_t ticket) {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = subs_.find(ticket);
+    if (it == subs_.end()) return RL_EINVAL;
+    Sub* s = it->second;
+    if (s->done) return RL_OK;
+    s->cancelled = true;
+    if (s->taken == 0) drop_locked(s, RL_ECANCELED);
+    else if (s->waiting) s->cv.notify_all();
+    return RL_OK;
+}
+
 int Coalescer::Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* rem, int64_t* retry,
-                    int64_t* reset, int64_t* done_ns) {
+                    int64_t* reset, int64_t* done_ns, rl_table_info* info) {
     std::unique_lock<std::mutex> lk(mu_);
     auto it = subs_.find(ticket);
     if (it == subs_.end()) return RL_EINVAL;
     Sub* s = it->second;
-    if (!s->done) {
-        s->waiting = true;
-        if (timeout_ns < 0) {
-            s->cv.wait(lk, [&] { return s->done; });
-        } else if (!s->cv.wait_for(lk, std::chrono::nanoseconds(timeout_ns), [&] { return s->done; })) {
+    const int64_t t_end = timeout_ns < 0 ? INT64_MAX : steady_ns() + timeout_ns;
+    int code = RL_OK;   // != RL_OK: the ticket ends without results
+    for (;;) {
+        if (s->cancelled) { code = RL_ECANCELED; break; }
+        if (s->done) {
+            if (s->dropped) code = s->status;
+            break;
+        }
+        const int64_t now = steady_ns();
+        if (s->deadline && now >= s->deadline) {
+            // not launched: never applied; launched: applied, results discarded
+            if (s->taken == 0) drop_locked(s, RL_EDEADLINE);
+            code = RL_EDEADLINE;
+            break;
+        }
+        if (now >= t_end) {
             s->waiting = false;
             return RL_ETIMEOUT;
         }
+        s->waiting = true;
+        const int64_t until = s->deadline ? std::min(t_end, s->deadline) : t_end;
+        if (until == INT64_MAX) s->cv.wait(lk);
+        else s->cv.wait_for(lk, std::chrono::nanoseconds(until - now));
     }
+    s->waiting = false;
     subs_.erase(it);
+    if (code != RL_OK) {
+        if (done_ns) *done_ns = steady_ns();
+        s->waited = true;
+        maybe_free_locked(s);
+        return code;
+    }
+    // done and applied: no slot or queue references it any more
     lk.unlock();
     const size_t m = s->m;
-    if (dec) memcpy(dec, s->dec, m);
-    if (rem) memcpy(rem, s->rem, 8 * m);
-    if (retry) memcpy(retry, s->retry, 8 * m);
-    if (reset) memcpy(reset, s->reset, 8 * m);
+    if (s->op == OP_REQ) {
+        if (dec) memcpy(dec, s->dec, m);
+        if (rem) memcpy(rem, s->rem, 8 * m);
+        if (retry) memcpy(retry, s->retry, 8 * m);
+        if (reset) memcpy(reset, s->reset, 8 * m);
+    }
+    if (info) *info = s->info;
     if (done_ns) *done_ns = s->done_ns;
     int st = s->status;
     put_sub(s);
@@ -344,7 +458,7 @@ void Coalescer::put_sub(Sub* s) {
 std::vector<BatchTrace> Coalescer::Trace() {
     std::lock_guard<std::mutex> g(mu_);
     std::vector<BatchTrace> out;
-    if (trace_.size() < trace_cap_) return trace_;
+    if (trace_cap_ == 0 || trace_.size() < trace_cap_) return trace_;
     const size_t h = done_batches_ % trace_cap_;
     out.insert(out.end(), trace_.begin() + h, trace_.end());
     out.insert(out.end(), trace_.begin(), trace_.begin() + h);
@@ -358,6 +472,87 @@ rl_coalescer_stats Coalescer::Stats() {
     return r;
 }
 
+int Coalescer::run_table_op(Sub* op) {
+    rl_table_info info{};
+    info.struct_size = sizeof info;
+    int st;
+    if (op->op == OP_INFO) {
+        st = be_->table_info(op->now_ms, &info);
+    } else {
+        st = be_->gc(op->now_ms, op->cap_tb, op->cap_win, &info);
+        std::lock_guard<std::mutex> g(mu_);
+        st_.gc_runs++;
+        if (st != RL_OK) st_.gc_failures++;
+    }
+    op->info = info;
+    return st;
+}
+
+// Automatic GC (include/rl_coalescer.h, rl_coalescer_opts.gc_*): every request
+// inserts at most one entry into one table (a window request may also move one
+// window key to the spill table), so after a count with `budget` free slots
+// below the high-water mark of the fullest table, that many requests cannot
+// push any table past it.  Runs before launching `s`, so a GC lands between
+// the batches launched before and `s`.
+void Coalescer::auto_gc(const Slot& s) {
+    if (o_.gc_interval_ns <= 0 || s.m == 0) return;
+    const int64_t now = steady_ns();
+    if (gc_counted_ && gc_launched_ + s.m <= gc_budget_ && now - gc_last_check_ < o_.gc_interval_ns) return;
+    // server clock of the GC: no later request may carry an older one (the
+    // engine's clock is floor(ts / 1e6)); requests come in near time order,
+    // within gc_margin_ms of each other
+    int64_t min_ts = INT64_MAX;
+    for (size_t i = 0; i < s.m; i++) min_ts = std::min(min_ts, s.ts[i]);
+    const int64_t now_ms = (min_ts >= 0 ? min_ts / 1000000 : -((-min_ts + 999999) / 1000000)) - o_.gc_margin_ms;
+    rl_table_info in{};
+    in.struct_size = sizeof in;
+    if (be_->table_info(now_ms, &in) != RL_OK) {
+        gc_counted_ = true;
+        gc_budget_ = 0;
+        gc_last_check_ = now;
+        gc_launched_ = 0;
+        return;
+    }
+    const double hi = o_.gc_high_pct / 100.0;
+    auto high = [&](uint64_t cap) { return (uint64_t)(hi * (double)cap); };
+    auto full = [&](uint64_t used, uint64_t cap) { return used + s.m > high(cap); };
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        st_.gc_checks++;
+    }
+    if (full(in.tb_used, in.tb_capacity) || full(in.win_used, in.win_capacity) ||
+        full(in.spill_used, in.spill_capacity)) {
+        // grow a table whose live keys alone fill half its headroom
+        auto grow = [&](uint64_t live, uint64_t cap, uint64_t lim) -> uint64_t {
+            if (live <= high(cap) / 2) return 0;
+            if (lim && 2 * cap > lim) return 0;
+            return 2 * cap;
+        };
+        const uint64_t ntb = grow(in.tb_live, in.tb_capacity, o_.gc_max_tb_capacity);
+        uint64_t nwin = grow(in.win_live, in.win_capacity, o_.gc_max_win_capacity);
+        if (!nwin && in.spill_live > high(in.spill_capacity) / 2 &&
+            !(o_.gc_max_win_capacity && 2 * in.win_capacity > o_.gc_max_win_capacity))
+            nwin = 2 * in.win_capacity;   // the spill table follows the window table
+        rl_table_info out{};
+        out.struct_size = sizeof out;
+        int st = be_->gc(now_ms, ntb, nwin, &out);
+        bool ok = st == RL_OK;
+        if (!ok && (ntb || nwin)) ok = be_->gc(now_ms, 0, 0, &out) == RL_OK;   // no room to grow: in place
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            st_.gc_runs++;
+            if (!ok) st_.gc_failures++;
+        }
+        if (ok) in = out;
+    }
+    auto room = [&](uint64_t used, uint64_t cap) -> uint64_t { return used < high(cap) ? high(cap) - used : 0; };
+    gc_budget_ = std::min({room(in.tb_used, in.tb_capacity), room(in.win_used, in.win_capacity),
+                           room(in.spill_used, in.spill_capacity)});
+    gc_counted_ = true;
+    gc_last_check_ = now;
+    gc_launched_ = 0;
+}
+
 void Coalescer::submitter() {
     for (;;) {
         std::unique_lock<std::mutex> lk(mu_);
@@ -365,56 +560,112 @@ void Coalescer::submitter() {
         cv_sub_.wait(lk, [&] { return (stop_ && pending_ == 0) || (pending_ > 0 && inflight_ < (int)o_.max_in_flight); });
         sub_idle_ = false;
         if (pending_ == 0) break;   // stop_ with nothing left
-        if (o_.linger_ns > 0 && inflight_ == 0 && pending_ < o_.max_batch && !stop_ && !queue_.front()->reset_op) {
+        // submissions dropped while queued (deadline, cancel) leave the queue here
+        auto pop_dropped = [&] {
+            while (!queue_.empty() && queue_.front()->dropped) {
+                Sub* d = queue_.front();
+                queue_.pop_front();
+                d->in_queue = false;
+                maybe_free_locked(d);
+            }
+        };
+        pop_dropped();
+        if (o_.linger_ns > 0 && inflight_ == 0 && pending_ < o_.max_batch && !stop_ && queue_.front()->op == OP_REQ) {
             const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(o_.linger_ns);
             sub_idle_ = true;
             cv_sub_.wait_until(lk, until, [&] { return stop_ || pending_ >= o_.max_batch; });
             sub_idle_ = false;
+            pop_dropped();
+            if (pending_ == 0) continue;
         }
-        if (queue_.front()->reset_op) {
-            // every request before it is launched; the backend's reset waits
-            // for them on the device, then applies the DEL
-            Sub* r = queue_.front();
+        Sub* f = queue_.front();
+        if (f->op == OP_INFO || f->op == OP_GC) {
+            // synchronous, on this thread: every batch before it is launched
+            // and the backend drains them; nothing after it is launched yet
             queue_.pop_front();
+            f->in_queue = false;
             pending_ -= 1;
-            r->taken = 1;
+            f->taken = 1;
             lk.unlock();
-            const int st = be_->reset(r->cfg[0], r->key[0], r->ts[0]);
+            const int st = run_table_op(f);
             lk.lock();
-            r->status = st;
-            r->left = 0;
-            r->done = true;
-            r->done_ns = steady_ns();
-            st_.decided += 1;
-            if (r->waiting) r->cv.notify_all();
+            f->status = st;
+            f->left = 0;
+            f->done = true;
+            f->done_ns = steady_ns();
+            if (f->waiting) f->cv.notify_all();
+            maybe_free_locked(f);
+            // a manual GC invalidates the automatic GC's count
+            gc_counted_ = false;
             continue;
         }
         const int si = next_slot_;
-        next_slot_ = (next_slot_ + 1) % (int)o_.max_in_flight;
         Slot& s = slots_[si];
         s.parts.clear();
+        s.is_reset = false;
         size_t m = 0;
-        while (m < o_.max_batch && !queue_.empty() && !queue_.front()->reset_op) {
-            Sub* sub = queue_.front();
-            const size_t take = std::min(sub->m - sub->taken, (size_t)o_.max_batch - m);
-            s.parts.push_back({sub, sub->taken, take, m});
-            sub->taken += take;
-            m += take;
-            if (sub->taken == sub->m) queue_.pop_front();
+        if (f->op == OP_RESET) {
+            // like a one-request batch: enqueued between the batches around it
+            queue_.pop_front();
+            f->in_queue = false;
+            f->taken = 1;
+            f->inflight = 1;
+            pending_ -= 1;
+            s.parts.push_back({f, 0, 1, 0});
+            s.is_reset = true;
+        } else {
+            const int64_t now = steady_ns();
+            while (m < o_.max_batch && !queue_.empty()) {
+                Sub* sub = queue_.front();
+                if (sub->dropped) {
+                    queue_.pop_front();
+                    sub->in_queue = false;
+                    maybe_free_locked(sub);
+                    continue;
+                }
+                if (sub->op != OP_REQ) break;
+                if (sub->taken == 0 && (sub->cancelled || (sub->deadline && sub->deadline <= now))) {
+                    // its context ended before it was sent: never applied
+                    drop_locked(sub, sub->cancelled ? RL_ECANCELED : RL_EDEADLINE);
+                    queue_.pop_front();
+                    sub->in_queue = false;
+                    maybe_free_locked(sub);
+                    continue;
+                }
+                const size_t take = std::min(sub->m - sub->taken, (size_t)o_.max_batch - m);
+                s.parts.push_back({sub, sub->taken, take, m});
+                sub->taken += take;
+                sub->inflight++;
+                m += take;
+                if (sub->taken == sub->m) {
+                    queue_.pop_front();
+                    sub->in_queue = false;
+                }
+            }
+            if (m == 0) continue;   // everything at the head was dropped
+            pending_ -= m;
         }
-        pending_ -= m;
+        next_slot_ = (next_slot_ + 1) % (int)o_.max_in_flight;
         inflight_++;
         lk.unlock();
         if (trace_cap_) s.t_form = steady_ns();
-        // the submissions' inputs are immutable after Submit: copy unlocked
-        for (const auto& p : s.parts) {
-            memcpy(s.key + p.at, p.sub->key + p.off, 8 * p.count);
-            memcpy(s.ts + p.at, p.sub->ts + p.off, 8 * p.count);
-            memcpy(s.n + p.at, p.sub->n + p.off, 8 * p.count);
-            memcpy(s.cfg + p.at, p.sub->cfg + p.off, 4 * p.count);
+        if (s.is_reset) {
+            const Sub* r = s.parts[0].sub;
+            s.m = 0;
+            s.status = be_->launch_reset(si, s, r->cfg[0], r->key[0], r->ts[0]);
+        } else {
+            // the submissions' inputs are immutable after Submit: copy unlocked
+            for (const auto& p : s.parts) {
+                memcpy(s.key + p.at, p.sub->key + p.off, 8 * p.count);
+                memcpy(s.ts + p.at, p.sub->ts + p.off, 8 * p.count);
+                memcpy(s.n + p.at, p.sub->n + p.off, 8 * p.count);
+                memcpy(s.cfg + p.at, p.sub->cfg + p.off, 4 * p.count);
+            }
+            s.m = m;
+            auto_gc(s);
+            gc_launched_ += m;
+            s.status = be_->launch(si, s);
         }
-        s.m = m;
-        s.status = be_->launch(si, s);
         if (trace_cap_) s.t_launched = steady_ns();
         lk.lock();
         st_.batches++;
@@ -424,6 +675,13 @@ void Coalescer::submitter() {
         cv_done_.notify_one();
     }
     std::lock_guard<std::mutex> g(mu_);
+    // only dropped submissions can be left in the queue
+    while (!queue_.empty()) {
+        Sub* d = queue_.front();
+        queue_.pop_front();
+        d->in_queue = false;
+        maybe_free_locked(d);
+    }
     sub_exited_ = true;
     cv_done_.notify_all();
 }
@@ -440,11 +698,13 @@ void Coalescer::completer() {
         Slot& s = slots_[si];
         const int64_t t_wait = trace_cap_ ? steady_ns() : 0;
         int st = s.status == RL_OK ? be_->wait(si, s) : s.status;
-        for (const auto& p : s.parts) {
-            memcpy(p.sub->dec + p.off, s.dec + p.at, p.count);
-            memcpy(p.sub->rem + p.off, s.rem + p.at, 8 * p.count);
-            memcpy(p.sub->retry + p.off, s.retry + p.at, 8 * p.count);
-            memcpy(p.sub->reset + p.off, s.reset + p.at, 8 * p.count);
+        if (!s.is_reset) {
+            for (const auto& p : s.parts) {
+                memcpy(p.sub->dec + p.off, s.dec + p.at, p.count);
+                memcpy(p.sub->rem + p.off, s.rem + p.at, 8 * p.count);
+                memcpy(p.sub->retry + p.off, s.retry + p.at, 8 * p.count);
+                memcpy(p.sub->reset + p.off, s.reset + p.at, 8 * p.count);
+            }
         }
         const int64_t now = steady_ns();
         bool wake;
@@ -460,16 +720,18 @@ void Coalescer::completer() {
                 else trace_[done_batches_ % trace_cap_] = t;
             }
             done_batches_++;
-            st_.decided += s.m;
+            st_.decided += s.is_reset ? 1 : s.m;
             for (const auto& p : s.parts) {
                 Sub* sub = p.sub;
                 if (st != RL_OK) sub->status = st;
                 sub->left -= p.count;
-                if (sub->left == 0) {
+                sub->inflight--;
+                if (sub->left == 0 && !sub->done) {
                     sub->done = true;
                     sub->done_ns = now;
                     if (sub->waiting) sub->cv.notify_all();
                 }
+                maybe_free_locked(sub);   // orphaned (its waiter gave up) and now complete
             }
         }
         if (wake) cv_sub_.notify_one();
@@ -489,8 +751,13 @@ struct rl_coalescer {
 rlc::Coalescer* rlc::unwrap(rl_coalescer* c) { return c ? c->c : nullptr; }
 
 static int create(std::unique_ptr<rlc::Backend> be, const rl_coalescer_opts* opts, rl_coalescer** out) {
+    if (!out) return RL_EINVAL;
     rl_coalescer_opts o{};
-    if (opts) o = *opts;
+    o.struct_size = sizeof o;
+    if (opts) {
+        if (opts->struct_size != sizeof(rl_coalescer_opts)) return RL_EINVAL;
+        o = *opts;
+    }
     auto* c = new rlc::Coalescer(std::move(be), o);
     int rc = c->start();
     if (rc != RL_OK) {
@@ -506,25 +773,21 @@ extern "C" int rl_coalescer_create(rl_engine* e, const rl_coalescer_opts* opts, 
     return create(rlc::make_gpu_backend(e), opts, out);
 }
 
+extern "C" int rl_coalescer_create_with_host_backend(const rl_coalescer_backend* be, const rl_coalescer_opts* opts,
+                                                     rl_coalescer** out) {
+    if (!be || be->struct_size != sizeof(rl_coalescer_backend) || !be->batch || !out) return RL_EINVAL;
+    return create(rlc::make_fn_backend(*be), opts, out);
+}
+
 extern "C" int rl_coalescer_create_with_backend(rl_batch_fn fn, void* user, const rl_coalescer_opts* opts,
                                                 rl_coalescer** out) {
-    if (!fn || !out) return RL_EINVAL;
-    return create(rlc::make_fn_backend(fn, nullptr, user), opts, out);
+    return rl_coalescer_create_with_backends(fn, nullptr, user, opts, out);
 }
 
 extern "C" int rl_coalescer_create_with_backends(rl_batch_fn fn, rl_reset_fn reset_fn, void* user,
                                                  const rl_coalescer_opts* opts, rl_coalescer** out) {
-    if (!fn || !out) return RL_EINVAL;
-    return create(rlc::make_fn_backend(fn, reset_fn, user), opts, out);
-}
-
-extern "C" int rl_coalescer_reset(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, uint32_t cfg_id) {
-    if (!c) return RL_EINVAL;
-    uint64_t t;
-    const int64_t one = 1;
-    int rc = c->c->Submit(1, &key_id, &ts_ns, &one, &cfg_id, &t, true);
-    if (rc != RL_OK) return rc;
-    return c->c->Wait(t, -1, nullptr, nullptr, nullptr, nullptr);
+    rl_coalescer_backend b{sizeof(rl_coalescer_backend), fn, reset_fn, nullptr, nullptr, user};
+    return rl_coalescer_create_with_host_backend(&b, opts, out);
 }
 
 extern "C" int rl_coalescer_destroy(rl_coalescer* c) {
@@ -534,10 +797,24 @@ extern "C" int rl_coalescer_destroy(rl_coalescer* c) {
     return RL_OK;
 }
 
+extern "C" int64_t rl_coalescer_now_ns(void) { return rlc::steady_ns(); }
+
 extern "C" int rl_coalescer_submit(rl_coalescer* c, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
                                    const int64_t* n, const uint32_t* cfg_id, uint64_t* ticket) {
     if (!c) return RL_EINVAL;
     return c->c->Submit(m, key_id, ts_ns, n, cfg_id, ticket);
+}
+
+extern "C" int rl_coalescer_submit_deadline(rl_coalescer* c, size_t m, const uint64_t* key_id, const int64_t* ts_ns,
+                                            const int64_t* n, const uint32_t* cfg_id, int64_t deadline_ns,
+                                            uint64_t* ticket) {
+    if (!c) return RL_EINVAL;
+    return c->c->Submit(m, key_id, ts_ns, n, cfg_id, ticket, deadline_ns);
+}
+
+extern "C" int rl_coalescer_cancel(rl_coalescer* c, uint64_t ticket) {
+    if (!c) return RL_EINVAL;
+    return c->c->Cancel(ticket);
 }
 
 extern "C" int rl_coalescer_wait(rl_coalescer* c, uint64_t ticket, int64_t timeout_ns, uint8_t* decision,
@@ -549,15 +826,58 @@ extern "C" int rl_coalescer_wait(rl_coalescer* c, uint64_t ticket, int64_t timeo
 extern "C" int rl_coalescer_decide(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, int64_t n, uint32_t cfg_id,
                                    uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
                                    int64_t* reset_at_ns) {
+    return rl_coalescer_decide_deadline(c, key_id, ts_ns, n, cfg_id, 0, decision, remaining, retry_after_ns,
+                                        reset_at_ns);
+}
+
+extern "C" int rl_coalescer_decide_deadline(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, int64_t n,
+                                            uint32_t cfg_id, int64_t deadline_ns, uint8_t* decision,
+                                            int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns) {
     if (!c) return RL_EINVAL;
     uint64_t t;
-    int rc = c->c->Submit(1, &key_id, &ts_ns, &n, &cfg_id, &t);
+    int rc = c->c->Submit(1, &key_id, &ts_ns, &n, &cfg_id, &t, deadline_ns);
     if (rc != RL_OK) return rc;
     return c->c->Wait(t, -1, decision, remaining, retry_after_ns, reset_at_ns);
 }
 
+extern "C" int rl_coalescer_reset(rl_coalescer* c, uint64_t key_id, int64_t ts_ns, uint32_t cfg_id) {
+    if (!c) return RL_EINVAL;
+    uint64_t t;
+    int rc = c->c->SubmitOp(rlc::OP_RESET, key_id, ts_ns, cfg_id, 0, 0, 0, &t);
+    if (rc != RL_OK) return rc;
+    return c->c->Wait(t, -1, nullptr, nullptr, nullptr, nullptr);
+}
+
+static int table_op(rl_coalescer* c, rlc::Op op, int64_t now_ms, uint64_t tb, uint64_t win, rl_table_info* out) {
+    uint64_t t;
+    int rc = c->c->SubmitOp(op, 0, 0, 0, now_ms, tb, win, &t);
+    if (rc != RL_OK) return rc;
+    rl_table_info info{};
+    rc = c->c->Wait(t, -1, nullptr, nullptr, nullptr, nullptr, nullptr, &info);
+    if (out && rc == RL_OK) {
+        const uint32_t n = out->struct_size;
+        info.struct_size = n;
+        memcpy(out, &info, std::min<size_t>(n, sizeof info));
+    }
+    return rc;
+}
+
+extern "C" int rl_coalescer_table_info(rl_coalescer* c, int64_t now_ms, rl_table_info* out) {
+    if (!c || !out || out->struct_size < 8) return RL_EINVAL;
+    return table_op(c, rlc::OP_INFO, now_ms, 0, 0, out);
+}
+
+extern "C" int rl_coalescer_gc(rl_coalescer* c, int64_t now_ms, uint64_t tb_capacity, uint64_t win_capacity,
+                               rl_table_info* out) {
+    if (!c || (out && out->struct_size < 8)) return RL_EINVAL;
+    return table_op(c, rlc::OP_GC, now_ms, tb_capacity, win_capacity, out);
+}
+
 extern "C" int rl_coalescer_get_stats(rl_coalescer* c, rl_coalescer_stats* out) {
-    if (!c || !out) return RL_EINVAL;
-    *out = c->c->Stats();
+    if (!c || !out || out->struct_size < 8) return RL_EINVAL;
+    rl_coalescer_stats s = c->c->Stats();
+    const uint32_t n = out->struct_size;
+    s.struct_size = n;
+    memcpy(out, &s, std::min<size_t>(n, sizeof s));
     return RL_OK;
 }

@@ -1,12 +1,13 @@
 // coalescer.hpp -- request coalescer in front of the decision engine
-// (include/rl_coalescer.h has the policy and ordering contract).
+// (include/rl_coalescer.h has the policy, ordering and context contract).
 //
 // The reference's Limiter.AllowN is one Redis EVAL per call
 // (tokenbucket.go:172, slidingwindow.go:164, fixedwindow.go:152); the north
 // star's BatchAllow path gathers concurrent calls into GPU batches
 // (SURVEY.md §8b, §8f rank 1).  Threads: callers submit and wait; one
-// submitter thread forms batches and launches them; one completer thread
-// waits for each launch in order and hands results back.
+// submitter thread forms batches and launches them (and runs the ordered
+// table operations); one completer thread waits for each launch in order and
+// hands results back.
 #pragma once
 
 #include <stdint.h>
@@ -34,6 +35,7 @@ struct Slot {
     int64_t* retry = nullptr;
     int64_t* reset = nullptr;
     size_t m = 0;
+    bool is_reset = false;   // a Reset (parts[0].sub), not requests
     int status = RL_OK;
     int64_t t_form = 0, t_h2d = 0, t_launched = 0;   // steady ns (batch trace)
     struct Part {
@@ -43,31 +45,46 @@ struct Slot {
     std::vector<Part> parts;
 };
 
-// where batches go: the GPU engine, or a synchronous host function (tests)
+// where batches go: the GPU engine, or synchronous host functions (tests)
 class Backend {
 public:
     virtual ~Backend() = default;
     virtual int init(int nslots, size_t max_batch, std::vector<Slot>* slots) = 0;
     virtual int launch(int slot, Slot& s) = 0;   // asynchronous
+    // Reset after every launched batch and before every later one,
+    // asynchronous like a launch (completes through wait(slot))
+    virtual int launch_reset(int slot, Slot& s, uint32_t cfg, uint64_t key, int64_t ts) = 0;
     virtual int wait(int slot, Slot& s) = 0;     // until launch `slot` completed
-    // Reset after every launched batch (the submitter thread; the GPU engine's
-    // rl_reset drains its queues first)
-    virtual int reset(uint32_t cfg, uint64_t key, int64_t ts) = 0;
+    // synchronous table operations (the GPU engine drains its batches first)
+    virtual int table_info(int64_t now_ms, rl_table_info* out) = 0;
+    virtual int gc(int64_t now_ms, uint64_t tb_cap, uint64_t win_cap, rl_table_info* out) = 0;
 };
 
 std::unique_ptr<Backend> make_gpu_backend(rl_engine* e);
-std::unique_ptr<Backend> make_fn_backend(rl_batch_fn fn, rl_reset_fn rfn, void* user);
+std::unique_ptr<Backend> make_fn_backend(const rl_coalescer_backend& b);
 
-// one submission: its requests (copied) and results
+enum Op : uint8_t { OP_REQ, OP_RESET, OP_INFO, OP_GC };
+
+// one submission: its requests (copied) and results, or one table operation
 struct Sub {
     uint64_t first = 0;
     size_t m = 0, taken = 0, left = 0;
     int status = RL_OK;
-    bool reset_op = false;        // a Reset (key[0], ts[0], cfg[0]), not requests
+    Op op = OP_REQ;
+    int64_t deadline = 0;         // steady ns; 0 = none
     bool done = false;
     bool waiting = false;         // a caller blocks on cv (else completion skips the wake)
+    bool cancelled = false;       // rl_coalescer_cancel before completion
+    bool dropped = false;         // completed unapplied (deadline / cancel before launch)
+    bool in_queue = false;        // queue_ still holds it (the submitter pops it)
+    bool waited = false;          // the caller released its ticket
+    uint32_t inflight = 0;        // slot parts launched, not completed
     int64_t done_ns = 0;          // steady clock at completion
     int64_t submit_ns = 0;        // steady clock at Submit (batch trace)
+    // OP_INFO / OP_GC arguments and result
+    int64_t now_ms = 0;
+    uint64_t cap_tb = 0, cap_win = 0;
+    rl_table_info info{};
     std::condition_variable cv;
     std::unique_ptr<uint8_t[]> mem;
     uint64_t* key;
@@ -97,10 +114,15 @@ public:
     ~Coalescer();
     int start();
     int Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
-               uint64_t* ticket, bool reset_op = false);
-    // done_ns (optional): steady-clock completion time of the submission
+               uint64_t* ticket, int64_t deadline = 0);
+    // a Reset / table count / table GC, queued in sequence order
+    int SubmitOp(Op op, uint64_t key, int64_t ts, uint32_t cfg, int64_t now_ms, uint64_t cap_tb,
+                 uint64_t cap_win, uint64_t* ticket);
+    int Cancel(uint64_t ticket);
+    // done_ns (optional): steady-clock completion time of the submission;
+    // info (optional): an OP_INFO / OP_GC result
     int Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* rem, int64_t* retry, int64_t* reset,
-             int64_t* done_ns = nullptr);
+             int64_t* done_ns = nullptr, rl_table_info* info = nullptr);
     rl_coalescer_stats Stats();
     void Shutdown();
     // the trace ring, oldest first (empty unless RL_COALESCER_TRACE is set)
@@ -109,6 +131,14 @@ public:
 private:
     void submitter();
     void completer();
+    // drop a submission none of whose requests was launched: done, unapplied
+    void drop_locked(Sub* s, int code);
+    // free a submission no one references any more (queue, slots, caller)
+    void maybe_free_locked(Sub* s);
+    // automatic GC before launching `s` (submitter thread, lock not held)
+    void auto_gc(const Slot& s);
+    // run a synchronous table operation (submitter thread, lock not held)
+    int run_table_op(Sub* op);
     // pooled submissions: no heap allocation (and no mmap / page faults for
     // large ones) per Submit in steady state
     Sub* get_sub(size_t m);
@@ -132,6 +162,11 @@ private:
     std::vector<BatchTrace> trace_;   // ring of trace_cap_ batches
     size_t trace_cap_ = 0;
     uint64_t done_batches_ = 0;
+    // automatic GC (submitter thread only)
+    int64_t gc_last_check_ = 0;       // steady ns
+    uint64_t gc_launched_ = 0;        // requests launched since the last count
+    uint64_t gc_budget_ = 0;          // requests that cannot fill any table past gc_high_pct
+    bool gc_counted_ = false;         // a first count was taken
     std::thread t_sub_, t_done_;
 };
 

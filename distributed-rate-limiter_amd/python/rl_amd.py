@@ -36,8 +36,16 @@ NOW_WALL = -(1 << 63)
 SMS_DEFAULT = -(1 << 63)
 
 
-class rl_opts(C.Structure):
+class _Sized(C.Structure):
+    """an ABI struct whose first field is struct_size (include/rl_engine.h)"""
+
+    def __init__(self, *args, **kw):
+        super().__init__(C.sizeof(self), *args, **kw)
+
+
+class rl_opts(_Sized):
     _fields_ = [
+        ("struct_size", C.c_uint32),
         ("device", C.c_int32),
         ("profile", C.c_int32),
         ("tb_capacity", C.c_uint64),
@@ -48,8 +56,10 @@ class rl_opts(C.Structure):
     ]
 
 
-class rl_stats(C.Structure):
+class rl_stats(_Sized):
     _fields_ = [
+        ("struct_size", C.c_uint32),
+        ("pad_", C.c_uint32),
         ("batches", C.c_uint64),
         ("decisions", C.c_uint64),
         ("last_segments", C.c_uint64),
@@ -73,28 +83,44 @@ class rll_result(C.Structure):
     ]
 
 
-class rl_table_info(C.Structure):
-    _fields_ = [(k, C.c_uint64) for k in ("tb_capacity", "tb_used", "tb_live", "win_capacity", "win_used",
+class rl_table_info(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("pad_", C.c_uint32)] + [(k, C.c_uint64) for k in ("tb_capacity", "tb_used", "tb_live", "win_capacity", "win_used",
                                           "win_live", "spill_capacity", "spill_used", "spill_live")]
 
 
-class rl_coalescer_opts(C.Structure):
+class rl_coalescer_opts(_Sized):
     _fields_ = [
+        ("struct_size", C.c_uint32),
         ("max_batch", C.c_uint32),
         ("max_in_flight", C.c_uint32),
+        ("gc_high_pct", C.c_uint32),
         ("linger_ns", C.c_int64),
         ("queue_cap", C.c_uint64),
+        ("gc_interval_ns", C.c_int64),
+        ("gc_margin_ms", C.c_int64),
+        ("gc_max_tb_capacity", C.c_uint64),
+        ("gc_max_win_capacity", C.c_uint64),
     ]
 
 
-class rl_coalescer_stats(C.Structure):
-    _fields_ = [(k, C.c_uint64) for k in ("submitted", "decided", "batches", "max_batch_seen", "pending")]
+class rl_coalescer_stats(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("pad_", C.c_uint32)] + [
+        (k, C.c_uint64) for k in ("submitted", "decided", "batches", "max_batch_seen", "pending", "expired",
+                                  "cancelled", "gc_runs", "gc_checks", "gc_failures")]
 
 
 vp = C.c_void_p
 # rl_batch_fn (include/rl_coalescer.h)
 BATCH_FN = C.CFUNCTYPE(C.c_int, vp, C.c_size_t, vp, vp, vp, vp, vp, vp, vp, vp)
 RESET_FN = C.CFUNCTYPE(C.c_int, vp, C.c_uint32, C.c_uint64, C.c_int64)
+INFO_FN = C.CFUNCTYPE(C.c_int, vp, C.c_int64, C.POINTER(rl_table_info))
+GC_FN = C.CFUNCTYPE(C.c_int, vp, C.c_int64, C.c_uint64, C.c_uint64, C.POINTER(rl_table_info))
+
+
+class rl_coalescer_backend(_Sized):
+    _fields_ = [("struct_size", C.c_uint32), ("batch", BATCH_FN), ("reset", RESET_FN), ("table_info", INFO_FN),
+                ("gc", GC_FN), ("user", vp)]
+
 _sig = {
     "rl_engine_create": (C.c_int, [C.POINTER(rl_opts), C.POINTER(vp)]),
     "rl_engine_destroy": (C.c_int, [vp]),
@@ -103,6 +129,7 @@ _sig = {
     "rl_decide_batch_device": (C.c_int, [vp, C.c_size_t] + [vp] * 11),
     "rl_engine_sync": (C.c_int, [vp]),
     "rl_reset": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_int64]),
+    "rl_reset_device": (C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_int64, vp]),
     "rl_engine_stats": (C.c_int, [vp, C.POINTER(rl_stats)]),
     "rl_engine_set_timing": (C.c_int, [vp, C.c_int]),
     "rl_table_info_get": (C.c_int, [vp, C.c_int64, C.POINTER(rl_table_info)]),
@@ -140,7 +167,16 @@ _sig = {
     "rl_coalescer_create_with_backend": (C.c_int, [BATCH_FN, vp, C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_create_with_backends": (C.c_int, [BATCH_FN, RESET_FN, vp, C.POINTER(rl_coalescer_opts),
                                                     C.POINTER(vp)]),
+    "rl_coalescer_create_with_host_backend": (C.c_int, [C.POINTER(rl_coalescer_backend),
+                                                        C.POINTER(rl_coalescer_opts), C.POINTER(vp)]),
     "rl_coalescer_reset": (C.c_int, [vp, C.c_uint64, C.c_int64, C.c_uint32]),
+    "rl_coalescer_now_ns": (C.c_int64, []),
+    "rl_coalescer_submit_deadline": (C.c_int, [vp, C.c_size_t, vp, vp, vp, vp, C.c_int64, C.POINTER(C.c_uint64)]),
+    "rl_coalescer_cancel": (C.c_int, [vp, C.c_uint64]),
+    "rl_coalescer_decide_deadline": (C.c_int, [vp, C.c_uint64, C.c_int64, C.c_int64, C.c_uint32, C.c_int64,
+                                               vp, vp, vp, vp]),
+    "rl_coalescer_table_info": (C.c_int, [vp, C.c_int64, C.POINTER(rl_table_info)]),
+    "rl_coalescer_gc": (C.c_int, [vp, C.c_int64, C.c_uint64, C.c_uint64, C.POINTER(rl_table_info)]),
     "rl_hash_keys_host": (C.c_int, [C.c_size_t, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_char_p, C.c_size_t, vp]),
     "rl_coalescer_destroy": (C.c_int, [vp]),
     "rl_coalescer_submit": (C.c_int, [vp, C.c_size_t, vp, vp, vp, vp, C.POINTER(C.c_uint64)]),
@@ -203,7 +239,8 @@ class Engine:
 
     def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
                  max_batch=1 << 20, device=0, flags=0, spill_capacity=0):
-        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, flags, spill_capacity)
+        o = rl_opts(device=device, profile=profile, tb_capacity=tb_capacity, win_capacity=win_capacity,
+                    max_batch=max_batch, flags=flags, spill_capacity=spill_capacity)
         h = vp()
         rc = lib.rl_engine_create(C.byref(o), C.byref(h))
         if rc != RL_OK:
@@ -483,7 +520,8 @@ class LimiterEngine:
 
     def __init__(self, profile=PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1 << 16,
                  max_batch=1 << 16, device=0):
-        o = rl_opts(device, profile, tb_capacity, win_capacity, max_batch, 0, 0)
+        o = rl_opts(device=device, profile=profile, tb_capacity=tb_capacity, win_capacity=win_capacity,
+                    max_batch=max_batch)
         h = vp()
         buf = C.create_string_buffer(512)
         rc = lib.rll_engine_new(C.byref(o), C.byref(h), buf, 512)
@@ -600,36 +638,53 @@ def new_limiter(engine: LimiterEngine | None, algorithm, limit, window_ns, prefi
     return RateLimiter(h)
 
 
-RL_EAGAIN, RL_ECLOSED = -11, -32
+RL_EAGAIN, RL_ECLOSED, RL_EDEADLINE, RL_ECANCELED = -11, -32, -62, -125
+
+
+def now_ns() -> int:
+    """the coalescer's deadline clock (rl_coalescer_now_ns: CLOCK_MONOTONIC)"""
+    return lib.rl_coalescer_now_ns()
 
 
 class Coalescer:
     """rl_coalescer (include/rl_coalescer.h): concurrent submissions gathered
     into engine batches.  `engine` is an Engine (GPU) or, for the CPU tests of
     the batching logic, a Python function with rl_decide_batch's host-array
-    signature (the test seam rl_coalescer_create_with_backend)."""
+    signature (the test seam rl_coalescer_create_with_host_backend; `reset`,
+    `table_info`, `gc`: the other backend functions, optional).
 
-    def __init__(self, engine, max_batch=65536, max_in_flight=3, linger_ns=0, queue_cap=0, reset=None):
-        o = rl_coalescer_opts(max_batch, max_in_flight, linger_ns, queue_cap)
+    gc_interval_ns > 0 turns on the automatic table GC (rl_coalescer_opts)."""
+
+    def __init__(self, engine, max_batch=65536, max_in_flight=3, linger_ns=0, queue_cap=0, reset=None,
+                 table_info=None, gc=None, gc_interval_ns=0, gc_high_pct=0, gc_margin_ms=0,
+                 gc_max_tb_capacity=0, gc_max_win_capacity=0):
+        o = rl_coalescer_opts(max_batch=max_batch, max_in_flight=max_in_flight, gc_high_pct=gc_high_pct,
+                              linger_ns=linger_ns, queue_cap=queue_cap, gc_interval_ns=gc_interval_ns,
+                              gc_margin_ms=gc_margin_ms, gc_max_tb_capacity=gc_max_tb_capacity,
+                              gc_max_win_capacity=gc_max_win_capacity)
         h = vp()
         if isinstance(engine, Engine):
             rc = lib.rl_coalescer_create(engine.h, C.byref(o), C.byref(h))
-            self._fn = None
+            self._be = None
         else:
-            self._fn = BATCH_FN(engine)   # kept alive with the coalescer
-            self._rfn = RESET_FN(reset) if reset else C.cast(None, RESET_FN)
-            rc = lib.rl_coalescer_create_with_backends(self._fn, self._rfn, None, C.byref(o), C.byref(h))
+            # the callbacks live as long as the coalescer
+            self._be = rl_coalescer_backend(
+                batch=BATCH_FN(engine), reset=RESET_FN(reset) if reset else C.cast(None, RESET_FN),
+                table_info=INFO_FN(table_info) if table_info else C.cast(None, INFO_FN),
+                gc=GC_FN(gc) if gc else C.cast(None, GC_FN), user=None)
+            rc = lib.rl_coalescer_create_with_host_backend(C.byref(self._be), C.byref(o), C.byref(h))
         if rc != RL_OK:
             raise EngineError(rc, "rl_coalescer_create failed")
         self.h = h
 
-    def submit(self, key, ts, n, cfg) -> int:
+    def submit(self, key, ts, n, cfg, deadline_ns=0) -> int:
         key = np.ascontiguousarray(key, dtype=np.uint64)
         ts = np.ascontiguousarray(ts, dtype=np.int64)
         n = np.ascontiguousarray(n, dtype=np.int64)
         cfg = np.ascontiguousarray(cfg, dtype=np.uint32)
         t = C.c_uint64()
-        rc = lib.rl_coalescer_submit(self.h, key.size, _ptr(key), _ptr(ts), _ptr(n), _ptr(cfg), C.byref(t))
+        rc = lib.rl_coalescer_submit_deadline(self.h, key.size, _ptr(key), _ptr(ts), _ptr(n), _ptr(cfg),
+                                              deadline_ns, C.byref(t))
         if rc != RL_OK:
             raise EngineError(rc, "rl_coalescer_submit failed")
         return t.value
@@ -639,14 +694,27 @@ class Coalescer:
         rc = lib.rl_coalescer_wait(self.h, ticket, timeout_ns, *[_ptr(x) for x in out])
         return rc, out
 
-    def decide(self, key, ts, n, cfg):
+    def cancel(self, ticket: int) -> int:
+        return lib.rl_coalescer_cancel(self.h, ticket)
+
+    def decide(self, key, ts, n, cfg, deadline_ns=0):
         d, rem, retry, reset = C.c_uint8(), C.c_int64(), C.c_int64(), C.c_int64()
-        rc = lib.rl_coalescer_decide(self.h, key, ts, n, cfg, C.byref(d), C.byref(rem), C.byref(retry),
-                                     C.byref(reset))
+        rc = lib.rl_coalescer_decide_deadline(self.h, key, ts, n, cfg, deadline_ns, C.byref(d), C.byref(rem),
+                                              C.byref(retry), C.byref(reset))
         return rc, (d.value, rem.value, retry.value, reset.value)
 
     def reset(self, key, ts, cfg) -> int:
         return lib.rl_coalescer_reset(self.h, key, ts, cfg)
+
+    def table_info(self, now_ms):
+        out = rl_table_info()
+        rc = lib.rl_coalescer_table_info(self.h, now_ms, C.byref(out))
+        return rc, out
+
+    def gc(self, now_ms, tb_capacity=0, win_capacity=0):
+        out = rl_table_info()
+        rc = lib.rl_coalescer_gc(self.h, now_ms, tb_capacity, win_capacity, C.byref(out))
+        return rc, out
 
     def stats(self) -> rl_coalescer_stats:
         st = rl_coalescer_stats()

@@ -14,8 +14,19 @@ Semantics per RPC follow the Go limiter (internal/ratelimiter):
     RetryAfter 0, ResetAt} (tokenbucket.go:100-112 and twins), fail-closed:
     UNAVAILABLE "failed to check rate limit: <err>";
   * keys are FormatKey(prefix, key) (config.go:81-87; prefix "" -> "ratelimit"),
-    hashed to the engine's key ids on the host (rl_hash_keys_host), one
-    namespace per limiter instance.
+    hashed to the engine's key ids on the host (rl_hash_keys_host).  As in
+    Redis, the formatted key is the only namespace: two limiters with one
+    prefix share state (a fixed and a sliding window of one length share
+    their window counters, fixedwindow.go:139-141 / slidingwindow.go:150-152);
+    --isolate-limiters gives every limiter a namespace of its own instead;
+  * contexts (interface.go:75): the RPC deadline becomes the coalescer
+    submission's deadline -- a request still queued when it passes is never
+    applied -- and an expired or cancelled request takes the error branch
+    (fail-open result, or DEADLINE_EXCEEDED / CANCELLED "failed to check rate
+    limit: context ...");
+  * the tables are collected from the serving path: the coalescer counts and
+    GCs them between batches (rl_coalescer_opts.gc_*), so a long-running
+    server never fills them.
 
 Run: python rl_server.py --port 8080 --limiter api:token_bucket:20:12s ...
 """
@@ -109,11 +120,12 @@ class RateLimiterService:
     backend).  `register(alg, limit, window_ns) -> cfg_id` registers a config
     with the backend; `clock()` -> Unix ns (time.Now())."""
 
-    def __init__(self, limiters, coalescer, register, clock=time.time_ns):
+    def __init__(self, limiters, coalescer, register, clock=time.time_ns, isolate=False):
         self.a = rl_grpc.api("ratelimiter.proto")
         self.h = rl_grpc.api("health.proto")
         self.co = coalescer
         self.clock = clock
+        self.isolate = isolate
         self.by_name = {}
         for lim in limiters:
             lim.cfg_id = register(lim.alg, lim.limit, lim.window_ns)
@@ -127,33 +139,52 @@ class RateLimiterService:
             ctx.abort(grpc.StatusCode.NOT_FOUND, f"unknown limiter {name!r}")
         return lim
 
+    def _ids(self, lim, keys, m) -> np.ndarray:
+        """FormatKey(prefix, key) hashed: the formatted key is the namespace
+        (Redis), or one namespace per limiter with --isolate-limiters"""
+        return rl_amd.hash_keys_host(keys, KEY_SEED, lim.prefix, cfg=[lim.cfg_id] * m if self.isolate else None)
+
+    def _key_id(self, lim, key: str) -> int:
+        return int(self._ids(lim, [key.encode()], 1)[0])
+
     @staticmethod
-    def _key_id(lim, key: str) -> int:
-        kb = key.encode()
-        data = np.frombuffer(kb, np.uint8).copy() if kb else np.zeros(1, np.uint8)
-        off = np.array([0, len(kb)], np.uint64)
-        return int(rl_amd.hash_keys_host((data, off), KEY_SEED, lim.prefix, cfg=[lim.cfg_id])[0])
+    def _deadline(ctx) -> int:
+        """the RPC deadline on the coalescer's clock (0 = none)"""
+        rem = ctx.time_remaining() if ctx is not None else None
+        if rem is None or rem > 1e6:   # no deadline (gRPC reports an infinite one as huge)
+            return 0
+        return max(1, rl_amd.now_ns() + int(rem * 1e9))
+
+    # rl_coalescer status -> (go error text, gRPC code) of the error branch
+    _CTX_ERR = {rl_amd.RL_EDEADLINE: ("context deadline exceeded", grpc.StatusCode.DEADLINE_EXCEEDED),
+                rl_amd.RL_ECANCELED: ("context canceled", grpc.StatusCode.CANCELLED)}
 
     def _result(self, lim, t, rc, dec, rem, retry, reset):
-        """AllowResponse, or the fail-closed error text"""
+        """AllowResponse, or (None, fail-closed error text, gRPC code)"""
         if rc == rl_amd.RL_OK and dec in (rl_amd.ALLOWED, rl_amd.DENIED):
             return self.a.AllowResponse(allowed=dec == rl_amd.ALLOWED, limit=lim.limit, remaining=rem,
-                                        retry_after_ns=retry, reset_at_unix_ns=reset), None
-        err = f"engine status {rc}" if rc != rl_amd.RL_OK else "script error (INCRBY overflow)"
+                                        retry_after_ns=retry, reset_at_unix_ns=reset), None, None
+        if rc in self._CTX_ERR:
+            err, code = self._CTX_ERR[rc]
+        else:
+            err = f"engine status {rc}" if rc != rl_amd.RL_OK else "script error (INCRBY overflow)"
+            code = grpc.StatusCode.UNAVAILABLE
         if lim.fail_open:
             return self.a.AllowResponse(allowed=True, limit=lim.limit, remaining=0, retry_after_ns=0,
-                                        reset_at_unix_ns=reset_at_ns(lim.alg, lim.limit, lim.window_ns, t)), None
-        return None, f"failed to check rate limit: {err}"
+                                        reset_at_unix_ns=reset_at_ns(lim.alg, lim.limit, lim.window_ns, t)), \
+                None, None
+        return None, f"failed to check rate limit: {err}", code
 
     def _allow_n(self, name, key, n, ctx):
         lim = self._limiter(name, ctx)
         if n <= 0:
             ctx.abort(grpc.StatusCode.INVALID_ARGUMENT, ERR_INVALID_N)
         t = self.clock()
-        rc, (dec, rem, retry, reset) = self.co.decide(self._key_id(lim, key), t, n, lim.cfg_id)
-        res, err = self._result(lim, t, rc, dec, rem, retry, reset)
+        rc, (dec, rem, retry, reset) = self.co.decide(self._key_id(lim, key), t, n, lim.cfg_id,
+                                                      deadline_ns=self._deadline(ctx))
+        res, err, code = self._result(lim, t, rc, dec, rem, retry, reset)
         if err:
-            ctx.abort(grpc.StatusCode.UNAVAILABLE, err)
+            ctx.abort(code, err)
         return res
 
     # -- RPCs ----------------------------------------------------------------
@@ -194,14 +225,13 @@ class RateLimiterService:
         if idx:
             kid = np.empty(len(idx), np.uint64)
             for name, pos in groups.items():
-                lim = self.by_name[name]
-                kid[pos] = rl_amd.hash_keys_host([keys[p] for p in pos], KEY_SEED, lim.prefix,
-                                                 cfg=[lim.cfg_id] * len(pos))
-            tk = self.co.submit(kid, np.full(len(idx), t, np.int64), np.array(ns, np.int64), np.array(cfg, np.uint32))
+                kid[pos] = self._ids(self.by_name[name], [keys[p] for p in pos], len(pos))
+            tk = self.co.submit(kid, np.full(len(idx), t, np.int64), np.array(ns, np.int64), np.array(cfg, np.uint32),
+                                deadline_ns=self._deadline(ctx))
             rc, (dec, rem, retry, reset) = self.co.wait(tk, len(idx))
             for j, i in enumerate(idx):
                 lim = self.by_name[rs[i].limiter]
-                res, err = self._result(lim, t, rc, int(dec[j]), int(rem[j]), int(retry[j]), int(reset[j]))
+                res, err, _ = self._result(lim, t, rc, int(dec[j]), int(rem[j]), int(retry[j]), int(reset[j]))
                 out[i] = res if res is not None else self.a.AllowResponse(error=err)
         return self.a.AllowBatchResponse(results=out)
 
@@ -235,8 +265,10 @@ class GpuBackend:
         self.register = self.eng.register
         self.co = None
 
-    def start(self, max_batch=1 << 16):
-        self.co = rl_amd.Coalescer(self.eng, max_batch=max_batch, max_in_flight=3)
+    def start(self, max_batch=1 << 16, gc_interval_ns=NS, gc_margin_ms=1000):
+        """the coalescer, with the tables collected from the serving path"""
+        self.co = rl_amd.Coalescer(self.eng, max_batch=max_batch, max_in_flight=3, gc_interval_ns=gc_interval_ns,
+                                   gc_margin_ms=gc_margin_ms)
         return self.co
 
     def close(self):
@@ -272,12 +304,19 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=1 << 16)
     ap.add_argument("--tb-capacity", type=int, default=1 << 22)
     ap.add_argument("--win-capacity", type=int, default=1 << 22)
+    ap.add_argument("--gc-interval-ms", type=float, default=1000.0,
+                    help="count the tables at least this often and collect expired keys (0 = never)")
+    ap.add_argument("--gc-margin-ms", type=int, default=1000,
+                    help="GC at the last request's clock minus this (request clocks may lag by this much)")
+    ap.add_argument("--isolate-limiters", action="store_true",
+                    help="one key namespace per limiter (the reference shares state between limiters with "
+                         "the same prefix, as Redis keys are the formatted strings)")
     args = ap.parse_args(argv)
     specs = args.limiter or ["default:token_bucket:20:12s"]
     limiters = [Limiter.parse(s) for s in specs]
     be = GpuBackend(args.device, args.tb_capacity, args.win_capacity, args.max_batch)
-    svc = RateLimiterService(limiters, None, be.register)
-    svc.co = be.start(args.max_batch)
+    svc = RateLimiterService(limiters, None, be.register, isolate=args.isolate_limiters)
+    svc.co = be.start(args.max_batch, int(args.gc_interval_ms * 1e6), args.gc_margin_ms)
     print(f"rate limiter gRPC server on {args.address}: " + ", ".join(specs), file=sys.stderr, flush=True)
     try:
         serve(svc, args.address, args.workers, ready=lambda p: print(f"READY {p}", flush=True))

@@ -16,6 +16,9 @@
  * during the call (the *_device entry point: until the stream reaches it); the
  * engine owns all device memory.  Calls on one engine are not re-entrant.
  * Every function returns RL_OK (0) or a negative RL_E* status.
+ * Every struct starts with `struct_size`, which the caller sets to sizeof the
+ * struct it was compiled with: inputs of a size the library does not know are
+ * rejected with RL_EINVAL, outputs are written up to the caller's size.
  */
 #ifndef RL_ENGINE_H
 #define RL_ENGINE_H
@@ -56,6 +59,7 @@ extern "C" {
 typedef struct rl_engine rl_engine;
 
 typedef struct rl_opts {
+    uint32_t struct_size;   /* sizeof(rl_opts) */
     int32_t  device;        /* HIP device ordinal */
     int32_t  profile;       /* RL_PROFILE_* */
     uint64_t tb_capacity;   /* token-bucket table slots; rounded up to a power of 2 */
@@ -79,6 +83,8 @@ typedef struct rl_opts {
 #define RL_OPT_PIPELINE 1u
 
 typedef struct rl_stats {
+    uint32_t struct_size;     /* sizeof(rl_stats) */
+    uint32_t pad_;
     uint64_t batches;
     uint64_t decisions;
     uint64_t last_segments;   /* distinct keys in the last batch */
@@ -130,14 +136,23 @@ int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* key_id, const
  * table filled, RL_EORDER, RL_ETIMEOUT) and clears it */
 int rl_engine_sync(rl_engine* e);
 
-/* Reset(ctx, key) at time ts_ns: DEL of the key(s) AllowN would touch at ts_ns */
+/* Reset(ctx, key) at time ts_ns: DEL of the key(s) AllowN would touch at ts_ns
+ * (tokenbucket.go:136-144, slidingwindow.go:125-139, fixedwindow.go:118-128).
+ * Synchronous. */
 int rl_reset(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns);
+/* The same DEL enqueued in batch order: after every batch enqueued before the
+ * call, before every batch enqueued after it (it runs on the engine's replay
+ * stream, nothing is drained); `stream` (a hipStream_t, NULL = the engine's
+ * stream) waits for it. */
+int rl_reset_device(rl_engine* e, uint32_t cfg_id, uint64_t key_id, int64_t ts_ns, void* stream);
 
 int rl_engine_stats(rl_engine* e, rl_stats* out);
 
 /* State-table occupancy.  A key is live at server clock now_ms when its Redis
  * TTL has not expired (a window entry: either of its two counter keys). */
 typedef struct rl_table_info {
+    uint32_t struct_size;     /* sizeof(rl_table_info) */
+    uint32_t pad_;
     uint64_t tb_capacity, tb_used, tb_live;
     uint64_t win_capacity, win_used, win_live;
     uint64_t spill_capacity, spill_used, spill_live;   /* spill slots ever claimed / live window keys */

@@ -39,6 +39,10 @@ class OracleStore:
         self.sim = oracle.OracleSim(oracle.REDIS7)
         self.fail = fail
         self.lock = threading.Lock()
+        self.gate = threading.Event()   # cleared: the store hangs (a busy engine)
+        self.gate.set()
+        self.entered = threading.Event()
+        self.applied = 0
 
     def register(self, alg, limit, window):
         return self.sim.add_config(alg, limit, window)
@@ -47,6 +51,9 @@ class OracleStore:
         import ctypes
         if self.fail:
             return rl_amd.RL_EDEVICE
+        self.entered.set()
+        self.gate.wait(30)
+        self.applied += m
 
         def arr(p, ct, dt):
             return np.ctypeslib.as_array((ct * m).from_address(p)).view(dt)
@@ -93,6 +100,12 @@ def cpu_server():
     stop.set()
     th.join(10)
     co.close()
+
+
+def _ns(svc, limiter, key):
+    """the Redis key identity: FormatKey(prefix, key) -- limiters with one
+    prefix share it (config.go:81-87)"""
+    return (svc.by_name[limiter].prefix, key)
 
 
 def _shadow(svc):
@@ -164,7 +177,7 @@ def test_decisions_equal_the_oracle(cpu_server):
             got = st.AllowBatch(svc.a.AllowBatchRequest(requests=reqs)).results
             t = clock_before + 1_250_000
             ok = [i for i, r in enumerate(reqs) if r.n > 0]
-            key = np.array([ids.setdefault((reqs[i].limiter, reqs[i].key), len(ids)) for i in ok], np.uint64)
+            key = np.array([ids.setdefault(_ns(svc, reqs[i].limiter, reqs[i].key), len(ids)) for i in ok], np.uint64)
             d, rem, retry, reset, _ = sim.decide(key, np.full(len(ok), t, np.int64),
                                                  np.array([reqs[i].n for i in ok], np.int64),
                                                  np.array([cid[reqs[i].limiter] for i in ok], np.uint32))
@@ -179,7 +192,7 @@ def test_decisions_equal_the_oracle(cpu_server):
             lim, key = names[rng.integers(len(names))], f"u{rng.integers(6)}"
             g = st.Allow(svc.a.AllowRequest(limiter=lim, key=key))
             t = clock_before + 1_250_000
-            d, rem, retry, reset, _ = sim.decide([ids.setdefault((lim, key), len(ids))], [t], [1], [cid[lim]])
+            d, rem, retry, reset, _ = sim.decide([ids.setdefault(_ns(svc, lim, key), len(ids))], [t], [1], [cid[lim]])
             assert (g.allowed, g.remaining, g.retry_after_ns, g.reset_at_unix_ns) == \
                 (bool(d[0]), rem[0], retry[0], reset[0]), step
 
@@ -245,7 +258,7 @@ def test_grpc_on_the_gpu_engine():
                     for _ in range(rng.integers(1, 50))]
             t = svc.clock.t + 1_250_000
             got = st.AllowBatch(svc.a.AllowBatchRequest(requests=reqs)).results
-            key = np.array([ids.setdefault((r.limiter, r.key), len(ids)) for r in reqs], np.uint64)
+            key = np.array([ids.setdefault(_ns(svc, r.limiter, r.key), len(ids)) for r in reqs], np.uint64)
             d, rem, retry, reset, _ = sim.decide(key, np.full(len(reqs), t, np.int64),
                                                  np.array([r.n for r in reqs], np.int64),
                                                  np.array([cid[r.limiter] for r in reqs], np.uint32))
@@ -254,7 +267,135 @@ def test_grpc_on_the_gpu_engine():
                     (bool(d[j]), rem[j], retry[j], reset[j]), (step, j)
             if step % 10 == 9:
                 st.Reset(svc.a.ResetRequest(limiter="fw", key="u1"))
-                sim.reset(cid["fw"], ids.setdefault(("fw", "u1"), len(ids)), svc.clock.t)
+                sim.reset(cid["fw"], ids.setdefault(_ns(svc, "fw", "u1"), len(ids)), svc.clock.t)
+    finally:
+        ch.close()
+        stop.set()
+        th.join(10)
+        be.close()
+
+
+class FakeCtx:
+    """a servicer context with a deadline time_remaining() seconds away"""
+
+    def __init__(self, remaining):
+        self.remaining = remaining
+
+    def time_remaining(self):
+        return self.remaining
+
+    def abort(self, code, details):
+        raise grpc.RpcError(code, details)
+
+
+@pytest.mark.parametrize("fail_open", [True, False])
+def test_expired_context_takes_the_error_branch(fail_open):
+    """interface_test.go:267-275: a context already done -> error (fail-closed)
+    or the fail-open result; the store never sees the request"""
+    store = OracleStore()
+    spec = "t:token_bucket:10:10s::" + ("true" if fail_open else "false")
+    svc = rl_server.RateLimiterService([rl_server.Limiter.parse(spec)], None, store.register, clock=Clock())
+    svc.co = rl_amd.Coalescer(store.batch, max_batch=64, reset=store.reset)
+    try:
+        if fail_open:
+            r = svc.Allow(svc.a.AllowRequest(limiter="t", key="a"), FakeCtx(0.0))
+            assert (r.allowed, r.limit, r.remaining, r.retry_after_ns) == (True, 10, 0, 0)
+        else:
+            with pytest.raises(grpc.RpcError) as e:
+                svc.Allow(svc.a.AllowRequest(limiter="t", key="a"), FakeCtx(0.0))
+            assert e.value.args == (grpc.StatusCode.DEADLINE_EXCEEDED,
+                                    "failed to check rate limit: context deadline exceeded")
+        # AllowBatch: per-request errors
+        rs = svc.AllowBatch(svc.a.AllowBatchRequest(requests=[svc.a.AllowNRequest(limiter="t", key="b", n=1)]),
+                            FakeCtx(0.0)).results
+        assert rs[0].allowed if fail_open else rs[0].error.endswith("context deadline exceeded")
+        assert store.applied == 0
+        # a live context is served
+        r = svc.Allow(svc.a.AllowRequest(limiter="t", key="a"), FakeCtx(5.0))
+        assert r.allowed and r.remaining == 9 and store.applied == 1
+    finally:
+        svc.co.close()
+
+
+def test_short_deadlines_under_load_are_never_applied():
+    """RPCs with a 50 ms deadline queue behind a hung store: the clients get
+    DEADLINE_EXCEEDED, the requests are dropped before launch, and later
+    decisions equal the oracle over the applied requests only"""
+    store = OracleStore()
+    svc = rl_server.RateLimiterService([rl_server.Limiter.parse("tb:token_bucket:5:60s")], None, store.register,
+                                       clock=Clock())
+    svc.co = rl_amd.Coalescer(store.batch, max_batch=64, max_in_flight=1, reset=store.reset)
+    ch, stop, th = start(svc)
+    try:
+        st = rl_grpc.rate_limiter_stub(ch)
+        store.gate.clear()
+        first = st.Allow.future(svc.a.AllowRequest(limiter="tb", key="k"))   # holds the store
+        assert store.entered.wait(10)
+        errs = []
+        for _ in range(6):
+            try:
+                st.AllowN(svc.a.AllowNRequest(limiter="tb", key="k", n=2), timeout=0.05)
+            except grpc.RpcError as e:
+                errs.append(e.code())
+        assert errs == [grpc.StatusCode.DEADLINE_EXCEEDED] * 6
+        import time
+        time.sleep(0.1)   # every server-side deadline has passed
+        store.gate.set()
+        assert first.result(10).remaining == 4
+        r = st.Allow(svc.a.AllowRequest(limiter="tb", key="k"))
+        assert r.allowed and r.remaining == 3      # none of the 6 x n=2 was applied
+        s = svc.co.stats()
+        assert s.expired == 6 and store.applied == 2
+    finally:
+        ch.close()
+        stop.set()
+        th.join(10)
+        svc.co.close()
+
+
+class FastClock(Clock):
+    """time.Now() advancing 30 ms per read: keys expire during the run"""
+
+    def __call__(self):
+        with self.lock:
+            self.t += 30_000_000
+            return self.t
+
+
+@pytest.mark.gpu
+def test_grpc_gc_many_more_keys_than_slots():
+    """the server collects its tables itself: 4096-slot tables, far more
+    distinct keys over the run, every decision equal to the oracle"""
+    lims = ["g1:token_bucket:5:1s", "g2:fixed_window:4:1s", "g3:sliding_window:3:1s:other"]
+    be = rl_server.GpuBackend(0, 4096, 4096, 1 << 13)
+    svc = rl_server.RateLimiterService([rl_server.Limiter.parse(s) for s in lims], None, be.register,
+                                       clock=FastClock())
+    svc.co = be.start(1 << 13, gc_interval_ns=10 ** 12, gc_margin_ms=100)
+    ch, stop, th = start(svc)
+    try:
+        st = rl_grpc.rate_limiter_stub(ch)
+        sim, cid = _shadow(svc)
+        ids = {}
+        rng = np.random.default_rng(9)
+        base = 0
+        for step in range(160):
+            reqs = [svc.a.AllowNRequest(limiter=lims[rng.integers(3)].split(":")[0],
+                                        key=f"u{base + rng.integers(2000)}", n=int(rng.choice([1, 2])))
+                    for _ in range(rng.integers(200, 500))]
+            base += 220
+            t = svc.clock.t + 30_000_000
+            got = st.AllowBatch(svc.a.AllowBatchRequest(requests=reqs)).results
+            key = np.array([ids.setdefault(_ns(svc, r.limiter, r.key), len(ids)) for r in reqs], np.uint64)
+            d, rem, retry, reset, _ = sim.decide(key, np.full(len(reqs), t, np.int64),
+                                                 np.array([r.n for r in reqs], np.int64),
+                                                 np.array([cid[r.limiter] for r in reqs], np.uint32))
+            for j, g in enumerate(got):
+                assert not g.error, (step, j, g.error)
+                assert (g.allowed, g.remaining, g.retry_after_ns, g.reset_at_unix_ns) == \
+                    (bool(d[j]), rem[j], retry[j], reset[j]), (step, j)
+        s = svc.co.stats()
+        assert len(ids) > 4 * 2 * 4096
+        assert s.gc_runs >= 2 and s.gc_failures == 0
     finally:
         ch.close()
         stop.set()
