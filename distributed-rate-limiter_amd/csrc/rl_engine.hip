@@ -347,6 +347,32 @@ __global__ void k_reset(uint64_t key, int64_t ts, const CfgDev* cfgs, uint32_t c
     if (c.alg == ALG_SLIDING_WINDOW) wk_delete(&win[s], spill, ws - c.ttl_c);
 }
 
+// Redis KEYS (rl_table_keys): every live key of the three tables
+__device__ inline void key_emit(rl_key_rec* out, uint64_t cap, unsigned long long* cnt, uint64_t k, int64_t ws,
+                                uint32_t kind) {
+    const unsigned long long i = atomicAdd(cnt, 1ull);
+    if (i < cap) out[i] = rl_key_rec{k, ws, kind, 0};
+}
+__global__ void k_table_keys(const TbEntry* tb, uint64_t ntb, const WinEntry* win, uint64_t nwin,
+                             const SpillEntry* sp, uint64_t nsp, int64_t now_ms, int32_t profile, rl_key_rec* out,
+                             uint64_t cap, unsigned long long* cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntb + nwin + nsp; i += stride) {
+        if (i < ntb) {
+            if (entry_live(tb[i], now_ms, profile)) key_emit(out, cap, cnt, tb[i].key, 0, RL_KIND_HASH);
+        } else if (i < ntb + nwin) {
+            const WinEntry& x = win[i - ntb];
+            if (x.key == EMPTY_KEY) continue;
+            for (int k = 0; k < 2; k++)
+                if (x.s[k].when != ABSENT && key_alive(x.s[k].when, now_ms, profile))
+                    key_emit(out, cap, cnt, x.key, x.s[k].ws, RL_KIND_WINDOW);
+        } else {
+            const SpillEntry& x = sp[i - ntb - nwin];
+            if (entry_live(x, now_ms, profile)) key_emit(out, cap, cnt, x.key, x.ws, RL_KIND_WINDOW);
+        }
+    }
+}
+
 // diagnostic timestamp (10 ns ticks) into *w
 __global__ void k_stamp(uint32_t* w) { *w = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
@@ -1161,6 +1187,34 @@ extern "C" int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* ou
     if (!ok) return fail(e, RL_EDEVICE, "table count failed");
     return copy_out(out, rl_table_info{sizeof(rl_table_info), 0, e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3],
                                        e->spill_cap, h[4], h[5]});
+}
+
+extern "C" int rl_table_keys(rl_engine* e, int64_t now_ms, rl_key_rec* out, size_t cap, uint64_t* count) {
+    if (!e || !count || (cap && !out)) return RL_EINVAL;
+    (void)hipSetDevice(e->device);
+    int r = drain(e);
+    if (r != RL_OK) return r;
+    unsigned long long* d = nullptr;
+    rl_key_rec* dout = nullptr;
+    HIPCHK(e, hipMalloc(&d, sizeof(unsigned long long)));
+    if (cap && hipMalloc(&dout, sizeof(rl_key_rec) * cap) != hipSuccess) {
+        (void)hipFree(d);
+        return fail(e, RL_ENOMEM, "table keys: allocation failed");
+    }
+    hipStream_t s = e->stream;
+    unsigned long long n = 0;
+    bool ok = hipMemsetAsync(d, 0, sizeof n, s) == hipSuccess;
+    k_table_keys<<<1024, 256, 0, s>>>(e->d_tb, e->tb_cap, e->d_win, e->win_cap, e->d_spill, e->spill_cap, now_ms,
+                                       e->profile, dout, cap, d);
+    ok = ok && hipMemcpyAsync(&n, d, sizeof n, hipMemcpyDeviceToHost, s) == hipSuccess;
+    ok = ok && hipStreamSynchronize(s) == hipSuccess;
+    if (ok && cap && n)
+        ok = hipMemcpy(out, dout, sizeof(rl_key_rec) * std::min<uint64_t>(n, cap), hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d);
+    (void)hipFree(dout);
+    if (!ok) return fail(e, RL_EDEVICE, "table keys failed");
+    *count = n;
+    return RL_OK;
 }
 
 extern "C" int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, uint64_t win_capacity,

@@ -157,16 +157,19 @@ Engine::~Engine() {
     if (e_) rl_engine_destroy(e_);
 }
 
-uint64_t Engine::Intern(uint32_t ns, const std::string& formatted_key) {
-    std::string k = std::to_string(ns);
-    k.push_back('\0');
-    k += formatted_key;
+uint64_t Engine::Intern(const std::string& formatted_key) {
     std::lock_guard<std::mutex> g(intern_mu_);
-    auto it = ids_.find(k);
+    auto it = ids_.find(formatted_key);
     if (it != ids_.end()) return it->second;
-    uint64_t id = next_id_++;
-    ids_.emplace(std::move(k), id);
+    uint64_t id = names_.size();
+    ids_.emplace(formatted_key, id);
+    names_.push_back(formatted_key);
     return id;
+}
+
+std::string Engine::Name(uint64_t id) {
+    std::lock_guard<std::mutex> g(intern_mu_);
+    return id < names_.size() ? names_[id] : std::string();
 }
 
 // ---------------------------------------------------------------------------
@@ -183,7 +186,7 @@ std::string engine_error(rl_engine* e, int rc) {
 class GpuLimiter final : public RateLimiter {
 public:
     GpuLimiter(Engine* eng, Config cfg, uint32_t cfg_id, int32_t alg)
-        : eng_(eng), cfg_(std::move(cfg)), cfg_id_(cfg_id), ns_(eng->NewNamespace()),
+        : eng_(eng), cfg_(std::move(cfg)), cfg_id_(cfg_id),
           host_cfg_(rl::make_cfg(alg, cfg_.Limit, cfg_.Window)) {}
 
     const Config& config() const override { return cfg_; }
@@ -223,7 +226,7 @@ public:
                 t = clock_now;
             }
             size_t k = live.size();
-            key[k] = eng_->Intern(ns_, cfg_.FormatKey(reqs[i].key));
+            key[k] = eng_->Intern(cfg_.FormatKey(reqs[i].key));
             ts[k] = t;
             n[k] = reqs[i].n;
             sms[k] = eng_->server_ms_override != INT64_MIN ? eng_->server_ms_override
@@ -285,7 +288,7 @@ public:
         (void)ctx;
         if (closed_.load())
             return Error::New(Error::Other, "failed to reset rate limit: engine: client is closed");
-        uint64_t id = eng_->Intern(ns_, cfg_.FormatKey(key));
+        uint64_t id = eng_->Intern(cfg_.FormatKey(key));
         std::lock_guard<std::mutex> g(eng_->mu());
         int rc = rl_reset(eng_->raw(), cfg_id_, id, t);
         if (rc != RL_OK)
@@ -308,7 +311,6 @@ private:
     Engine* eng_;
     Config cfg_;
     uint32_t cfg_id_;
-    uint32_t ns_;
     rl::CfgDev host_cfg_;
     std::atomic<bool> closed_{false};
 };
@@ -440,6 +442,30 @@ extern "C" int rll_engine_set_server_ms(rll_engine* e, int64_t server_ms) {
     if (!e) return RLL_ERR_ARG;
     e->eng->server_ms_override = server_ms;
     return RLL_OK;
+}
+
+extern "C" int rll_keys(rll_engine* e, int64_t server_ms, char* buf, size_t len) {
+    if (!e || (len && !buf)) return -RLL_ERR_ARG;
+    std::vector<rl_key_rec> recs(64);
+    uint64_t n = 0;
+    for (;;) {
+        std::lock_guard<std::mutex> g(e->eng->mu());
+        if (rl_table_keys(e->eng->raw(), server_ms, recs.data(), recs.size(), &n) != RL_OK) return -RLL_ERR_FAILED;
+        if (n <= recs.size()) break;
+        recs.resize(n);
+    }
+    std::vector<std::string> names;
+    for (uint64_t i = 0; i < n; i++) {
+        std::string b = e->eng->Name(recs[i].key_id);
+        // a window key: fmt.Sprintf("%s:%d", FormatKey(key), ws) (fixedwindow.go:139-141)
+        if (recs[i].kind == RL_KIND_WINDOW) b += ":" + std::to_string(recs[i].window_start);
+        names.push_back(std::move(b));
+    }
+    std::sort(names.begin(), names.end());
+    std::string out;
+    for (auto& x : names) out += x + "\n";
+    if (len) snprintf(buf, len, "%s", out.c_str());
+    return (int)out.size();
 }
 
 extern "C" int rll_config_validate(const char* algorithm, int64_t limit, int64_t window_ns, char* err,

@@ -99,15 +99,19 @@ struct Context {
 using Clock = std::function<int64_t()>;
 int64_t WallClockNs();
 
-// One GPU engine plus the key-id interner: the "storage" all limiters share.
+// One GPU engine plus the key-id interner: the "storage" all limiters share,
+// as one Redis.  A key's identity is its formatted name (FormatKey,
+// config.go:81-87) and nothing else, so limiters with one Prefix share state
+// exactly as they share Redis keys.
 class Engine {
 public:
     static Error Create(const rl_opts& opts, std::unique_ptr<Engine>* out);
     explicit Engine(rl_engine* e) : e_(e) {}
     ~Engine();
     rl_engine* raw() { return e_; }
-    uint64_t Intern(uint32_t ns, const std::string& formatted_key);
-    uint32_t NewNamespace() { return next_ns_.fetch_add(1); }
+    uint64_t Intern(const std::string& formatted_key);
+    // the formatted key of an interned id ("" if unknown)
+    std::string Name(uint64_t id);
     std::mutex& mu() { return mu_; }
     Clock clock = WallClockNs;
     // test hook: when >= 0, every call passes this Redis clock (ms)
@@ -118,8 +122,7 @@ private:
     std::mutex mu_;
     std::mutex intern_mu_;
     std::unordered_map<std::string, uint64_t> ids_;
-    uint64_t next_id_ = 0;
-    std::atomic<uint32_t> next_ns_{0};
+    std::vector<std::string> names_;   // by id
 };
 
 struct BatchRequest {

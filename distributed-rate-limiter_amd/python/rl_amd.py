@@ -144,6 +144,8 @@ _sig = {
     "rll_engine_free": (C.c_int, [vp]),
     "rll_engine_raw": (vp, [vp]),
     "rll_engine_set_server_ms": (C.c_int, [vp, C.c_int64]),
+    "rll_keys": (C.c_int, [vp, C.c_int64, C.c_char_p, C.c_size_t]),
+    "rl_table_keys": (C.c_int, [vp, C.c_int64, vp, C.c_size_t, C.POINTER(C.c_uint64)]),
     "rll_config_validate": (C.c_int, [C.c_char_p, C.c_int64, C.c_int64, C.c_char_p, C.c_size_t]),
     "rll_format_key": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_size_t]),
     "rll_duration_string": (C.c_int, [C.c_int64, C.c_char_p, C.c_size_t]),
@@ -531,6 +533,15 @@ class LimiterEngine:
 
     def set_server_ms(self, ms):
         lib.rll_engine_set_server_ms(self.h, SMS_DEFAULT if ms is None else ms)
+
+    def keys(self, server_ms):
+        """Redis KEYS: the live keys' formatted names, sorted (rll_keys)"""
+        n = lib.rll_keys(self.h, server_ms, None, 0)
+        if n < 0:
+            raise GoError(-n, "rll_keys failed")
+        buf = C.create_string_buffer(n + 1)
+        lib.rll_keys(self.h, server_ms, buf, n + 1)
+        return buf.value.decode().splitlines()
 
     def close(self):
         if self.h:

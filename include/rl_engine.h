@@ -159,6 +159,22 @@ typedef struct rl_table_info {
 } rl_table_info;
 int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* out);
 
+/* Redis KEYS: every key live at server clock now_ms, as (key id, kind,
+ * window start).  A token-bucket key is the hash FormatKey(key)
+ * (tokenbucket.go:95); a window key is FormatKey(key):ws (fixedwindow.go:139-141,
+ * slidingwindow.go:150-152).  Writes up to `cap` records (any order);
+ * *count = how many keys are live.  Synchronous, waits for queued batches; a
+ * diagnostic (the reference's tests list keys with miniredis Keys()). */
+#define RL_KIND_HASH   0
+#define RL_KIND_WINDOW 1
+typedef struct rl_key_rec {
+    uint64_t key_id;
+    int64_t window_start;   /* Unix seconds (RL_KIND_WINDOW); 0 for a hash */
+    uint32_t kind;          /* RL_KIND_* */
+    uint32_t pad_;
+} rl_key_rec;
+int rl_table_keys(rl_engine* e, int64_t now_ms, rl_key_rec* out, size_t cap, uint64_t* count);
+
 /* Table GC (the TTLs of tokenbucket.go:170,
  * slidingwindow.go:161-162, fixedwindow.go:151): drop every key expired at
  * server clock now_ms -- Redis's active expiry -- and optionally resize the

@@ -58,6 +58,13 @@ rl_engine* rll_engine_raw(rll_engine* e);
  * RLL_SMS_DEFAULT restores the default */
 int rll_engine_set_server_ms(rll_engine* e, int64_t server_ms);
 
+/* Redis KEYS (what the reference's tests read with miniredis Keys()): the
+ * live keys' names at Redis clock server_ms, sorted, one per line
+ * ("prefix:key" for a token bucket, "prefix:key:ws" for a window counter).
+ * Writes what fits in buf (NUL-terminated); returns the full length, or a
+ * negative RLL_ERR_* code. */
+int rll_keys(rll_engine* e, int64_t server_ms, char* buf, size_t len);
+
 /* Config.Validate() (config.go:16-50); algorithm NULL means a nil *Config */
 int rll_config_validate(const char* algorithm, int64_t limit, int64_t window_ns, char* err, size_t errlen);
 /* Config.FormatKey(key) (config.go:81-87) for a config with this Prefix

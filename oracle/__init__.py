@@ -59,6 +59,8 @@ def c_oracle():
         lib.rlo_tb_reset_at.argtypes = [C.c_int64, C.c_int64, C.c_double]
         lib.rlo_live_keys.restype = C.c_size_t
         lib.rlo_live_keys.argtypes = [vp, C.c_int64]
+        lib.rlo_keys.restype = C.c_size_t
+        lib.rlo_keys.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_size_t]
         _lib = lib
     return _lib
 
@@ -101,3 +103,10 @@ class OracleSim:
 
     def reset(self, cfg, key, ts, server_ms=0):
         self.lib.rlo_reset(self.h, cfg, key, ts, server_ms)
+
+    def keys(self, s_ms):
+        """live keys at server time s_ms: [(id, kind, ws)] (kind 0 hash, 1 window)"""
+        n = self.lib.rlo_keys(self.h, s_ms, None, None, None, 0)
+        ids, kind, ws = np.empty(n, np.uint64), np.empty(n, np.uint8), np.empty(n, np.int64)
+        self.lib.rlo_keys(self.h, s_ms, _p(ids), _p(kind), _p(ws), n)
+        return list(zip(ids.tolist(), kind.tolist(), ws.tolist()))

@@ -434,3 +434,21 @@ size_t rlo_live_keys(rlo_sim* s, int64_t s_ms) {
     }
     return k;
 }
+
+/* Redis KEYS at server time s_ms: up to cap (id, kind, ws) triples of live
+ * keys (miniredis Keys() in the reference's CustomPrefix tests); returns the
+ * number of live keys */
+size_t rlo_keys(rlo_sim* s, int64_t s_ms, uint64_t* id, uint8_t* kind, int64_t* ws, size_t cap) {
+    size_t k = 0;
+    for (size_t i = 0; i < s->cap; i++) {
+        ent_t* e = &s->tab[i];
+        if (!(e->used && e->present && !is_expired(s, e, s_ms))) continue;
+        if (k < cap) {
+            id[k] = e->id;
+            kind[k] = e->kind;
+            ws[k] = e->ws;
+        }
+        k++;
+    }
+    return k;
+}

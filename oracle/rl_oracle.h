@@ -87,6 +87,9 @@ double  rlo_tb_refill_rate(int64_t limit, int64_t w_ns);
 int64_t rlo_tb_reset_at(int64_t limit, int64_t w_ns, double now);
 /* number of live keys in the simulated keyspace at server time s_ms */
 size_t  rlo_live_keys(rlo_sim* s, int64_t s_ms);
+/* the live keys themselves: (id, kind 0 hash / 1 window, ws), up to cap;
+ * returns how many are live */
+size_t  rlo_keys(rlo_sim* s, int64_t s_ms, uint64_t* id, uint8_t* kind, int64_t* ws, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -68,8 +68,9 @@ class _OracleLimiter:
         self.closed = False
 
     def _key(self, key):
-        k = "%d\0%s:%s" % (id(self), self.prefix, key)   # FormatKey, per-limiter namespace
-        return self.be.intern(k)
+        # FormatKey (config.go:81-87): the formatted name is the key's only
+        # identity, so limiters with one prefix share it, as in Redis
+        return self.be.intern("%s:%s" % (self.prefix, key))
 
     def allow(self, key):
         return self.allow_n(key, 1)
@@ -117,6 +118,11 @@ class OracleBackend:
     def intern(self, k):
         return self._ids.setdefault(k, len(self._ids))
 
+    def keys(self):
+        """miniredis Keys(): the live keys' names, sorted"""
+        names = {v: k for k, v in self._ids.items()}
+        return sorted(names[i] + (":%d" % ws if kind == 1 else "") for i, kind, ws in self.sim.keys(self.clock.ff_ms))
+
     def new(self, algorithm, limit, window, prefix="", fail_open=False):
         return _OracleLimiter(self, algorithm, limit, window, prefix, fail_open)
 
@@ -162,3 +168,6 @@ class GpuBackend:
 
     def new(self, algorithm, limit, window, prefix="", fail_open=False):
         return _GpuLimiter(self, self.rl.new_limiter(self.eng, algorithm, limit, window, prefix, fail_open))
+
+    def keys(self):
+        return self.eng.keys(self.clock.ff_ms)

@@ -16,10 +16,6 @@ MINUTE = 60 * NS
 SEC = NS
 
 
-def _prefix_ok(be, prefix):
-    return True
-
-
 # ----------------------------------------------------------------- fixed window
 def fw_allow(be):  # fixedwindow_integration_test.go:27-65
     lim = be.new("fixed_window", 5, MINUTE)
@@ -266,6 +262,65 @@ def tb_max_capacity(be):  # tokenbucket_integration_test.go:432-462
     assert r.Allowed and r.Remaining == 9
 
 
+# ------------------------------------------------------------- key names
+def _minute_start(t):
+    return t // NS // 60 * 60      # Truncate(time.Minute): year 1 is minute-aligned with the Unix epoch
+
+
+def fw_custom_prefix(be):  # fixedwindow_integration_test.go:307-333
+    lim = be.new("fixed_window", 5, MINUTE, prefix="custom")
+    assert lim.allow("test-key").Allowed
+    keys = be.keys()
+    assert len(keys) == 1 and "custom:" in keys[0]
+    assert keys == ["custom:test-key:%d" % _minute_start(be.clock.t)]   # fixedwindow.go:139-141
+
+
+def sw_custom_prefix(be):  # slidingwindow_integration_test.go:340-368
+    lim = be.new("sliding_window", 5, MINUTE, prefix="custom")
+    assert lim.allow("test-key").Allowed
+    keys = be.keys()
+    assert len(keys) >= 1 and all("custom:" in k for k in keys)
+    # EXPIRE on the missing previous-window key is a no-op: one key
+    assert keys == ["custom:test-key:%d" % _minute_start(be.clock.t)]   # slidingwindow.go:150-152
+
+
+def tb_custom_prefix(be):  # tokenbucket_integration_test.go:369-395
+    lim = be.new("token_bucket", 5, MINUTE, prefix="custom")
+    assert lim.allow("test-key").Allowed
+    keys = be.keys()
+    assert len(keys) == 1 and "custom:" in keys[0]
+    assert keys == ["custom:test-key"]                                 # tokenbucket.go:95
+
+
+def prefix_isolation(be):  # builder scenario: FormatKey namespaces (config.go:81-87)
+    a = be.new("token_bucket", 5, MINUTE, prefix="custom")
+    b = be.new("token_bucket", 5, MINUTE)                  # "ratelimit" (config.go:62-64)
+    assert a.allow_n("k", 5).Remaining == 0
+    r = b.allow("k")
+    assert r.Allowed and r.Remaining == 4                   # ratelimit:k is another key
+    a.reset("k")                                            # DEL custom:k only
+    assert a.allow("k").Remaining == 4
+    assert b.allow("k").Remaining == 3
+    assert be.keys() == ["custom:k", "ratelimit:k"]
+
+
+def shared_prefix(be):  # builder scenario: two limiters, one prefix, one Redis key
+    a = be.new("token_bucket", 5, MINUTE)
+    b = be.new("token_bucket", 5, MINUTE)
+    assert a.allow_n("k", 3).Remaining == 2
+    r = b.allow_n("k", 2)
+    assert r.Allowed and r.Remaining == 0                   # the same bucket
+    assert not a.allow("k").Allowed
+    fw = be.new("fixed_window", 5, MINUTE, prefix="p")
+    sw = be.new("sliding_window", 5, MINUTE, prefix="p")
+    be.clock.t = (be.clock.t // MINUTE + 1) * MINUTE        # both in one window
+    assert fw.allow_n("w", 3).Remaining == 2
+    r = sw.allow("w")                                       # INCRBY on the same p:w:ws counter
+    assert r.Allowed and r.Remaining == 1
+    assert not fw.allow_n("w", 2).Allowed
+    assert be.keys() == ["p:w:%d" % _minute_start(be.clock.t), "ratelimit:k"]
+
+
 ALL = [
     ("fw_allow", fw_allow), ("fw_allow_n", fw_allow_n),
     ("fw_invalid_n", lambda be: invalid_n(be, "fixed_window")),
@@ -289,4 +344,7 @@ ALL = [
     ("tb_continuous_refill", tb_continuous_refill), ("tb_max_capacity", tb_max_capacity),
     ("tb_fail_open", lambda be: fail_open(be, "token_bucket")),
     ("tb_fail_closed", lambda be: fail_closed(be, "token_bucket")),
+    ("fw_custom_prefix", fw_custom_prefix), ("sw_custom_prefix", sw_custom_prefix),
+    ("tb_custom_prefix", tb_custom_prefix),
+    ("prefix_isolation", prefix_isolation), ("shared_prefix", shared_prefix),
 ]
