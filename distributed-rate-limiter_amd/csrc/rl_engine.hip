@@ -499,8 +499,6 @@ struct rl_engine {
     int perm_grid = 1024;       // k_permute / k_unpermute blocks at most
     uint32_t heavy_min = 32;    // segments this long replay cooperatively
     uint32_t huge_min = 4096;   // token-bucket segments this long are dequeued first
-    bool scatter_unpermute = false;   // RL_SCATTER_UNPERMUTE: the direct-scatter k_unpermute (A/B)
-    int probe_r = 1;                  // RL_PROBE_R: requests per k_probe thread (1 or 4; A/B: equal or 1 ahead)
     // dynamic LDS that makes a k_tb_chain block fill its CU's LDS: with two
     // batches in flight, the other batches' grouping and finish kernels (each launched with
     // GROUP_LDS bytes at least) then never share a CU with a chain
@@ -522,7 +520,6 @@ struct rl_engine {
     bool timing = false;
     bool timing_all = false;    // level 2: every stage; level 1: the replay only (2 events per batch)
     bool stamps = false;        // RL_STAMP_KERNELS: timestamps around each replay (debug words 18, 19)
-    bool bind_events = true;    // replay timing events bound to the dispatch (RL_EV_MARKERS: marker packets)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::array<hipEvent_t, 8>> ev_pending;
     double stage_ms[NSTAGES] = {0, 0, 0, 0, 0};
@@ -606,7 +603,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     // front_done / chain_done only order the engine's own streams on this
     // device: a device-scope release (no system-scope cache writeback per
     // batch); back_done hands results to the caller and keeps the default
-    const unsigned inner = hipEventDisableTiming | (getenv("RL_EV_SYSFENCE") ? 0u : hipEventReleaseToDevice);
+    const unsigned inner = hipEventDisableTiming | hipEventReleaseToDevice;
     ok &= hipEventCreateWithFlags(&B.front_done, inner) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.back_done, hipEventDisableTiming) == hipSuccess;
     ok &= hipEventCreateWithFlags(&B.chain_done, inner) == hipSuccess;
@@ -753,9 +750,6 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
         if (hipMalloc(&e->stamp_ring, 4 * 6 * STAMP_RING) != hipSuccess) return bail(RL_ENOMEM);
         if (hipMemset(e->stamp_ring, 0, 4 * 6 * STAMP_RING) != hipSuccess) return bail(RL_EDEVICE);
     }
-    e->scatter_unpermute = getenv("RL_SCATTER_UNPERMUTE") != nullptr;
-    e->bind_events = getenv("RL_EV_MARKERS") == nullptr;
-    if (const char* v = getenv("RL_PROBE_R")) e->probe_r = atoi(v) == 1 ? 1 : 4;
     {
         int dev_lds = 0;
         (void)hipDeviceGetAttribute(&dev_lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, e->device);
@@ -824,7 +818,7 @@ static hipEvent_t take_event(rl_engine* e) {
     }
     // timestamps only: a device-scope release
     hipEvent_t ev;
-    (void)hipEventCreateWithFlags(&ev, getenv("RL_EV_SYSFENCE") ? 0u : hipEventReleaseToDevice);
+    (void)hipEventCreateWithFlags(&ev, hipEventReleaseToDevice);
     return ev;
 }
 
@@ -909,15 +903,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     uint32_t* ghist = B.ctrl + CTRL_HIST;
     // few enough blocks that the per-block histogram flush (3 x 256 global
     // atomics per block on 768 shared words) stays cheap
-    const int pr = e->probe_r;
-    int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK * pr - 1) / (PROBE_BLOCK * pr), (uint32_t)e->probe_grid);
-    if (pr == 4)
-        k_probe<4><<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
-                                                       e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
-                                                       e->win_base, e->invalid_key, B.sk0, ghist,
-                                                       e->sort_passes, a, B.rec, e->d_eflags);
-    else
-        k_probe<1><<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
+    const int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, (uint32_t)e->probe_grid);
+    k_probe<1><<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
                                                        e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
                                                        e->win_base, e->invalid_key, B.sk0, ghist,
                                                        e->sort_passes, a, B.rec, e->d_eflags);
@@ -951,7 +938,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
     // front_done rides on k_permute's dispatch packet (no marker packet)
     // unless a stamp kernel follows it
-    const bool bind_front = e->bind_events && !sr;
+    const bool bind_front = !sr;
     hipExtLaunchKernelGGL(k_permute, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                           bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base, e->d_cfg,
                           e->profile, B.rec, ps, pre);
@@ -966,14 +953,14 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // replay timing: the two events ride on the replay's own dispatch packet
     // (hipExtLaunchKernel) instead of two marker packets around it, unless
     // the stamp kernels must sit inside the timed interval
-    const bool bound_ev = e->timing && !e->stamps && !sr && e->bind_events;
+    const bool bound_ev = e->timing && !e->stamps && !sr;
     if (e->timing && !bound_ev) (void)hipEventRecord(ev[4], c);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 18);
     if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 2);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
     // timing off: chain_done rides on the dispatch instead
-    const bool bind_done = !e->timing && !e->stamps && !sr && e->bind_events;
+    const bool bind_done = !e->timing && !e->stamps && !sr;
     const hipEvent_t ev_a = bound_ev ? ev[4] : nullptr, ev_b = bound_ev ? ev[5] : bind_done ? B.chain_done : nullptr;
     if (ncfg <= (uint32_t)MAX_LCFG)
         hipExtLaunchKernelGGL(k_tb_chain<true>, dim3(e->coop_grid), dim3(CH_BLOCK), (uint32_t)e->chain_pad[0], c, ev_a, ev_b,
@@ -1003,7 +990,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 4);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
-    if (m <= UP_MAX && !e->scatter_unpermute) {
+    if (m <= UP_MAX) {
         // results to the caller's order through arrival-index buckets: no
         // scattered partial-line stores
         k_unpermute_bucket<<<(m + 256 * UP_ITEMS - 1) / (256 * UP_ITEMS), 256, GROUP_LDS, t>>>(

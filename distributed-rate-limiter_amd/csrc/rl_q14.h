@@ -105,24 +105,6 @@ RL_INLINE int64_t round_scaled(double a, int k) {
     return round_scaled_ge(a, k, 0.0, ge);
 }
 
-// Correctly rounded d / P for an integer-valued d in [1, 2^53) and P = 10^k,
-// 1 <= k <= 22 (exact), R = RN(1/P): one product, one Newton refinement, then
-// an exact midpoint test on the residual d - q*P (exact: q is within one ulp
-// of d/P).  Same result as IEEE division, a shorter dependent chain.
-RL_INLINE double div_pow10(double d, double P, double R) {
-    double q = d * R;
-    double r = __builtin_fma(-q, P, d);
-    q = __builtin_fma(r, R, q);
-    r = __builtin_fma(-q, P, d);
-    uint64_t b = dbits(q);
-    double qu = bitsd(b + 1), qd = bitsd(b - 1);
-    double hu = (qu - q) * P, hd = (q - qd) * P;     // exact: power of two times P
-    double r2 = r + r;
-    bool odd = b & 1;
-    if (r2 > hu || (r2 == hu && odd)) return qu;
-    if (-r2 > hd || (-r2 == hd && odd)) return qd;
-    return q;
-}
 
 // RNE(x * P) exactly, for x > 0, P = 10^k exact (k <= 22), x*P < 2^47
 #include "rl_pow5.h"

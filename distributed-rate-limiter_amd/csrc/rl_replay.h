@@ -243,33 +243,16 @@ struct TbEval {
     int64_t Dact;
 };
 
-// Exact-step formulations (A/B switches, both on by default; bit-identical):
-// RL_STEP_DIV  strtod("D e(E-13)") as one IEEE division D / 10^k (D < 2^47 and
-//              10^k, k <= 22, are exact doubles: Clinger's fast path) instead
-//              of rlq::div_pow10's corrected product
-// RL_STEP_RINT %.14g's digits as rint of the scaled sum plus a tie fix-up from
-//              the exact product residual (rl_tb_chain.h round_scaled_Pd)
-#ifndef RL_STEP_DIV
-#define RL_STEP_DIV 1
-#endif
-#ifndef RL_STEP_RINT
-#define RL_STEP_RINT 1
-#endif
-
 // the script step from a stored state given as digits Dpred in (mode, E)
 __device__ inline TbEval tb_eval(int mode, int64_t Dpred, int32_t E, double P, double R, bool alive, double add,
                                  double cap, double nd, int32_t profile) {
     TbEval v;
     double T;
     if (!alive) T = cap;
-    else if (mode == QM_DEC) {                                           // strtod("D e(E-13)")
-        if (RL_STEP_DIV) {
-            T = (double)Dpred / P;                                       // RN is sign-symmetric
-        } else {
-            const double t = rlq::div_pow10((double)(Dpred < 0 ? -Dpred : Dpred), P, R);
-            T = Dpred < 0 ? -t : t;
-        }
-    }
+    // strtod("D e(E-13)"): |D| < 2^47 and 10^k (k <= 22) are exact doubles,
+    // so one correctly rounded division is strtod's result (Clinger's fast
+    // path); RN is sign-symmetric
+    else if (mode == QM_DEC) T = (double)Dpred / P;
     else if (mode == QM_BIN) T = (double)Dpred * R;                      // exact: R = 2^E
     else T = tb_value(Dpred, E, profile);
     const double sum = T + add;

@@ -68,29 +68,13 @@ constexpr int CH_NE = 64;                              // near-list capacity per
 // with the mostly idle loader (wave 4) and the producers pair up on the
 // other three SIMDs.
 constexpr int CH_LOADER = 4;
-// RL_CH_IDLE: wave 8 (the chain's SIMD again) takes no work, so no producer
-// competes with the chain wave for that SIMD's issue slots
-#ifndef RL_CH_IDLE
-#define RL_CH_IDLE 0
-#endif
-constexpr int CH_IDLE = RL_CH_IDLE ? 8 : -1;
-static_assert(CH_NP + 2 + (RL_CH_IDLE ? 1 : 0) <= 16 && CH_NP >= 3 && (!RL_CH_IDLE || CH_NP >= 7), "wave roles");
+static_assert(CH_NP + 2 <= 16 && CH_NP >= 3, "wave roles");
 __device__ inline int ch_producer_index(uint32_t wave) {
-    if (wave == 0 || wave == (uint32_t)CH_LOADER || (int)wave == CH_IDLE) return -1;
-    return (int)wave - (wave < (uint32_t)CH_LOADER ? 1 : 2) - ((CH_IDLE >= 0 && (int)wave > CH_IDLE) ? 1 : 0);
+    if (wave == 0 || wave == (uint32_t)CH_LOADER) return -1;
+    return (int)wave - (wave < (uint32_t)CH_LOADER ? 1 : 2);
 }
-constexpr int CH_BLOCK = (CH_NP + 2 + (RL_CH_IDLE ? 1 : 0)) * 64;
-#ifndef RL_CH_SERIAL
-#define RL_CH_SERIAL 64
-#endif
-constexpr int CH_SERIAL = RL_CH_SERIAL;                // serial exact steps per round at most
-// serial steps go on until CH_LINGER steps past the last one that left the
-// regime: regime exits come in clusters (a balance random-walking across a
-// decade boundary or zero), and a serial step costs ~1/18 of a round
-#ifndef RL_CH_LINGER
-#define RL_CH_LINGER 0
-#endif
-constexpr uint32_t CH_LINGER = RL_CH_LINGER;
+constexpr int CH_BLOCK = (CH_NP + 2) * 64;
+constexpr int CH_SERIAL = 64;                          // serial exact steps per round at most
 // conservative scale of the allow/clamp threshold th*P (covers the rounding of
 // th*P and of the bound arithmetic with a wide margin)
 constexpr double CH_YSCALE = 1.0 - 0x1p-28;
@@ -131,15 +115,12 @@ struct ChState {
     uint32_t hot;       // diagnostics: segment of >= 65536 requests
 };
 
-// Speculative restart (RL_CH_SPEC): in a round whose chain window will
-// likely leave the regime, the producers predict the exit from nominal states
-// (the exit step q and the decade E of its result) and summarize the window
-// from q + 1 at scale 10^(13 - E) instead of the window after the chain's.
-// When the chain's exact exit and serial steps end at q + 1 in decade E, the
-// next round resolves that window at once -- no producers-only round.
-#ifndef RL_CH_SPEC
-#define RL_CH_SPEC 1
-#endif
+// Speculative restart: in a round whose chain window will likely leave the
+// regime, the producers predict the exit from nominal states (the exit step q
+// and the decade E of its result) and summarize the window from q + 1 at scale
+// 10^(13 - E) instead of the window after the chain's.  When the chain's
+// exact exit and serial steps end at q + 1 in decade E, the next round
+// resolves that window at once -- no producers-only round.
 struct ChSpec {
     uint32_t valid;
     uint32_t first, cnt;   // window [first, first + cnt), summarized in tile[buf]
@@ -157,7 +138,7 @@ struct ChainShared {
     uint16_t ne_rank[2][CH_NP][64];    // near steps of the tile before each producer lane
     int32_t ne_off[CH_NP * CH_NE];     // chain: resolved offset after each near step
     ChState st[2];
-    ChSpec spec[2];                    // producers' speculative window of the round (RL_CH_SPEC)
+    ChSpec spec[2];                    // producers' speculative window of the round
 };
 
 __device__ inline double ring_add(const ChainShared& sh, uint32_t p) {
@@ -309,7 +290,6 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
     const double p = x * P;
     const double err = __builtin_fma(x, P, -p);       // x*P == p + err exactly
     ge_lo = (p > (double)DEC_LO) | ((p == (double)DEC_LO) & (err >= 0.0));
-#if RL_STEP_RINT
     // RNE of p, then the exact product decides a tie of p: p - rint(p) is
     // +-1/2 exactly only when p's fraction is 1/2 (p < 2^52 has ulp <= 1/2),
     // and |err| <= ulp(p)/2 cannot move a non-tie across the half
@@ -318,13 +298,6 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
     d += ((h == 0.5) & (err > 0.0)) ? 1.0 : 0.0;
     d -= ((h == -0.5) & (err < 0.0)) ? 1.0 : 0.0;
     return d;
-#endif
-    const double d0 = floor(p);
-    const double f = p - d0;                          // exact
-    const bool odd = d0 * 0.5 != floor(d0 * 0.5);
-    // bitwise, not short-circuit: no branches in the chain's hot loop
-    const bool up = (f > 0.5) | ((f == 0.5) & ((err > 0.0) | ((err == 0.0) & odd)));
-    return up ? d0 + 1.0 : d0;
 }
 
 // The live-key step from stored digits Dpred (exact integer-valued double,
@@ -336,9 +309,8 @@ template <int MODE>
 __device__ inline double tb_step_d(double Dpred, double P, double R, double add, double th, double& tokens) {
     // strtod("D e(E-13)"): D < 2^47 and P = 10^k (k <= 22) are exact doubles,
     // so one correctly rounded IEEE division is strtod's result (Clinger's
-    // fast path); div_pow10 reaches the same value through a corrected product
-    const double T = MODE == QM_DEC ? (RL_STEP_DIV ? Dpred / P : rlq::div_pow10(Dpred, P, R))
-                                    : Dpred * R;                    // exact: R = 2^E
+    // fast path)
+    const double T = MODE == QM_DEC ? Dpred / P : Dpred * R;        // binary: exact, R = 2^E
     const double sum = T + add;
     tokens = sum;
     double Dn;
@@ -362,7 +334,7 @@ __device__ inline int32_t fast_mode(int64_t D, int32_t E, int32_t profile) {
 __device__ inline void mode_scale(int32_t mode, int32_t E, double& P, double& R) {
     if (mode == QM_DEC) {
         P = rlq::pow10_exact(13 - E);
-        R = RL_STEP_DIV ? 0.0 : 1.0 / P;   // the division step (RL_STEP_DIV) needs no reciprocal
+        R = 0.0;                           // the decimal step divides: no reciprocal
     } else {
         P = ldexp(1.0, -E);
         R = ldexp(1.0, E);
@@ -915,8 +887,8 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     // the key has expired: below th the step denies without clamping whatever
     // they are, so only those steps load them (from HBM)
     double avec = 0.0, tvec = 0.0;
-    uint32_t k = 0, kx = 0;   // kx: steps done when the last regime exit happened
-    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE || k < kx + CH_LINGER); k++) {
+    uint32_t k = 0;
+    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
         if ((k & 63u) == 0) {
             const uint32_t pq = q + lane;
             avec = pq < lim ? add_at(pq) : 0.0;
@@ -956,7 +928,7 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
                         D = v.tokens < 0.0 ? -(int64_t)Dn : (int64_t)Dn;
                         E = E + d;
                         Ps = P2;
-                        Rs = RL_STEP_DIV ? 0.0 : 1.0 / P2;
+                        Rs = 0.0;
                         nb = true;
                     }
                 }
@@ -969,9 +941,7 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
                 if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
             }
         }
-        const bool was_fast = mode != QM_NONE;
         mode = fast_mode(D, E, profile);
-        if (force || mode == QM_NONE || !was_fast || !same) kx = k + 1;   // this step left the regime
         q++;
     }
     return SerialOut{q, D, E, mode, k};
@@ -1234,7 +1204,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     lds_barrier();
     for (;;) {
         ChState s = sh.st[par];
-        if (RL_CH_SPEC) {
+        {
             const ChSpec sp = sh.spec[par];
             if (sp.valid) {
                 if (s.ccnt == 0 && s.mode == QM_DEC && s.pfirst == sp.first && s.E == sp.E) {
@@ -1272,13 +1242,13 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         CH_T(t0);
         if (ch_producer_index(wave) >= 0) {
             ChSpec sp{0u, 0u, 0u, 0u, 0};
-            if (RL_CH_SPEC && s.ccnt > 0 && s.mode == QM_DEC) sp = ch_predict(sh, s, P, R, j1);
+            if (s.ccnt > 0 && s.mode == QM_DEC) sp = ch_predict(sh, s, P, R, j1);
 #ifdef RL_STAMPS
             CH_T(t1);
             cyc[1] += t1 - t0;          // producers: the exit guess
             cyc[2] += sp.valid;         // producers: windows guessed
 #endif
-            if (RL_CH_SPEC && ch_producer_index(wave) == 0 && (threadIdx.x & 63) == 0) {
+            if (ch_producer_index(wave) == 0 && (threadIdx.x & 63) == 0) {
                 sp.buf = s.pbuf;
                 sh.spec[par ^ 1u] = sp;
             }
@@ -1305,8 +1275,6 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             CH_T(t1);
             cyc[0] += t1 - t0;
-        } else if ((int)wave == CH_IDLE) {
-            // no work: only the round barrier
         } else if (wave == (uint32_t)CH_LOADER) {
             const uint32_t first = s.ccnt ? s.cfirst : s.pfirst;
             ld_until(L, sh, first, s.pfirst + 2 * CH_W, j1, pre, lane);
