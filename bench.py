@@ -123,6 +123,32 @@ def cpu_baseline(workload, batch, per_core_sample):
                       f"timed region), after one untimed warm-up batch"}
 
 
+def cpu_config0(requests=1_000_000):
+    """BASELINE.md's configs[0] CPU line: Fixed Window
+    100/min, 10k uniform keys, a 1M-request trace, one request per call --
+    the reference's per-call path (one EVAL per Allow on one single-threaded
+    Redis) restated in C (oracle/rl_oracle.c, the cpu_baseline leg: test
+    infrastructure).  Every call is timed on its own (clock_gettime around
+    each): decisions/s and per-call p50 / p99 on one core."""
+    import oracle
+    gen = make_workload("fw_uniform", requests, 0)
+    sim = oracle.OracleSim(oracle.REDIS7)
+    for a, L, W in gen.configs:
+        sim.add_config(a, L, W)
+    key, ts, n, cfg = gen.next_batch()
+    t0 = time.perf_counter()
+    _, call_ns = sim.decide_timed(key, ts, n, cfg)
+    wall = time.perf_counter() - t0
+    return {"workload": WORKLOAD_DESC["fw_uniform"] + f", {requests} requests, one call per request",
+            "value": requests / wall, "unit": "decisions/s", "cores": 1, "kind": "port",
+            "p50_call_us": float(np.percentile(call_ns, 50)) / 1e3,
+            "p99_call_us": float(np.percentile(call_ns, 99)) / 1e3,
+            "mean_call_us": float(call_ns.mean()) / 1e3,
+            "how": "oracle/rl_oracle.c rlo_decide_timed: each request its own call, timed with CLOCK_MONOTONIC; "
+                   "the store is in-process (no Redis round trip or Lua VM: a lower bound on the reference's "
+                   "per-call latency)"}
+
+
 def e2e(args, out_fd):
     """BASELINE configs[4] through the native load generator (a child process;
     this process never touches the GPU)."""
@@ -627,6 +653,7 @@ def main():
         out["secondary"] = secondary
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(workload, args.batch, args.cpu_sample)
+        out["cpu_baseline"]["configs0"] = cpu_config0()
     if rank == 0:
         os.write(out_fd, (json.dumps(out) + "\n").encode())
     if dist.is_initialized():

@@ -59,6 +59,7 @@ def c_oracle():
         lib.rlo_tb_reset_at.argtypes = [C.c_int64, C.c_int64, C.c_double]
         lib.rlo_live_keys.restype = C.c_size_t
         lib.rlo_live_keys.argtypes = [vp, C.c_int64]
+        lib.rlo_decide_timed.argtypes = [vp, C.c_size_t] + [vp] * 9
         lib.rlo_keys.restype = C.c_size_t
         lib.rlo_keys.argtypes = [vp, C.c_int64, vp, vp, vp, C.c_size_t]
         _lib = lib
@@ -100,6 +101,19 @@ class OracleSim:
         self.lib.rlo_decide(self.h, m, _p(key), _p(ts), _p(n), _p(cfg), _p(sms), _p(dec), _p(rem),
                             _p(retry), _p(reset), _p(tok))
         return dec, rem, retry, reset, tok
+
+    def decide_timed(self, key, ts, n, cfg):
+        """one call per request, each timed: (decision, call_ns)"""
+        key = np.ascontiguousarray(key, np.uint64)
+        ts = np.ascontiguousarray(ts, np.int64)
+        n = np.ascontiguousarray(n, np.int64)
+        cfg = np.ascontiguousarray(cfg, np.uint32)
+        m = key.size
+        dec, rem, retry, reset, call = (np.empty(m, np.uint8), np.empty(m, np.int64), np.empty(m, np.int64),
+                                        np.empty(m, np.int64), np.empty(m, np.int64))
+        self.lib.rlo_decide_timed(self.h, m, _p(key), _p(ts), _p(n), _p(cfg), _p(dec), _p(rem), _p(retry),
+                                  _p(reset), _p(call))
+        return dec, call
 
     def reset(self, cfg, key, ts, server_ms=0):
         self.lib.rlo_reset(self.h, cfg, key, ts, server_ms)

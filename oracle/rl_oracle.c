@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define NS_PER_S 1000000000LL
 /* seconds from Jan 1 year 1 to the Unix epoch (Go's unixToInternal) */
@@ -451,4 +452,21 @@ size_t rlo_keys(rlo_sim* s, int64_t s_ms, uint64_t* id, uint8_t* kind, int64_t* 
         k++;
     }
     return k;
+}
+
+/* rlo_decide one request at a time with each call timed (CLOCK_MONOTONIC):
+ * per-call latency of the restated store for the cpu_baseline leg (the
+ * reference's per-call path: one EVAL per Allow).  call_ns[i] = the i-th
+ * call's duration. */
+void rlo_decide_timed(rlo_sim* s, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
+                      const uint32_t* cfg, uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                      int64_t* reset_at_ns, int64_t* call_ns) {
+    for (size_t i = 0; i < m; i++) {
+        struct timespec a, b;
+        clock_gettime(CLOCK_MONOTONIC, &a);
+        rlo_decide(s, 1, key + i, ts + i, n + i, cfg + i, NULL, decision + i, remaining + i, retry_after_ns + i,
+                   reset_at_ns + i, NULL);
+        clock_gettime(CLOCK_MONOTONIC, &b);
+        call_ns[i] = (int64_t)(b.tv_sec - a.tv_sec) * 1000000000LL + (b.tv_nsec - a.tv_nsec);
+    }
 }

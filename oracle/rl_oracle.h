@@ -73,6 +73,12 @@ void rlo_decide(rlo_sim* s, size_t m, const uint64_t* key, const int64_t* ts,
                 uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
                 int64_t* reset_at_ns, double* tokens);
 
+/* rlo_decide request by request, each call timed: call_ns[i] (the per-call
+ * latency of the restated path, for bench.py's cpu_baseline leg) */
+void rlo_decide_timed(rlo_sim* s, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
+                      const uint32_t* cfg, uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                      int64_t* reset_at_ns, int64_t* call_ns);
+
 /* Reset(ctx, key) at time ts (tokenbucket.go:136-144, slidingwindow.go:125-139,
  * fixedwindow.go:118-128): DEL of the keys the limiter would touch at ts. */
 void rlo_reset(rlo_sim* s, uint32_t cfg, uint64_t key, int64_t ts, int64_t server_ms);
