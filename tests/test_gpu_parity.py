@@ -258,6 +258,41 @@ def test_config3_mixed(rl):
     run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 19, win=1 << 20)
 
 
+def test_config3_per_gpu_scale(rl):
+    """BASELINE configs[3] at its per-GPU share: 1B keys hash-sharded over 8
+    GPUs is 125M keys per GPU.  Mixed tenants (cfg = key mod 3: TB 20/12s, SW
+    100/60s, FW 100/60s), 132M requests in 2M batches over ~132 s of virtual
+    time, tables sized for the share (TB 2^26, window 2^27 + spill 2^28: 18 GB
+    of HBM).  As configs[2]: a seeded 1/32 of the keys replayed by the oracle
+    bit for bit, and whole-run properties -- every request decided, the entries
+    used equal the distinct keys of each table, live spilled window keys."""
+    g = traces.MixedTenants(nkeys=125_000_000, batch=2_000_000)
+    eng = make_engine(rl, 0, tb=1 << 26, win=1 << 27, max_batch=1 << 21)
+    sim = oracle.OracleSim(0)
+    for c in g.configs:
+        assert eng.register(*c) == sim.add_config(*c)
+    seen = []
+    for b in range(66):
+        key, ts, n, cfg = g.next_batch()
+        res = eng.decide(key, ts, n, cfg, want_tokens=(b % 8 == 0))
+        assert np.all(res.decision <= 1), f"batch {b}"
+        pick = (key * np.uint64(0x9E3779B97F4A7C15) >> np.uint64(59)) == np.uint64(0)   # 1/32 of keys
+        ref = sim.decide(key[pick], ts[pick], n[pick], cfg[pick])
+        sub = rl.Decisions(res.decision[pick], res.remaining[pick], res.retry_after_ns[pick],
+                           res.reset_at_ns[pick], None if res.tokens is None else res.tokens[pick])
+        assert_same(sub, ref, g.configs, cfg[pick], what=f"batch {b}")
+        seen.append(np.unique(key))
+    allk = np.unique(np.concatenate(seen))
+    del seen
+    tb_keys = int(np.count_nonzero(allk % np.uint64(3) == np.uint64(0)))
+    info = eng.table_info(int(ts[-1]) // 1_000_000)
+    assert allk.size > 80_000_000
+    assert info.tb_used == tb_keys and info.win_used == allk.size - tb_keys
+    assert info.spill_used > 0 and info.spill_live > 0
+    assert eng.sync() == 0
+    eng.close()
+
+
 # --- per-key time going back (window keys beyond the 2-slot entry) -------------
 
 @pytest.mark.parametrize("profile", [0, 1])
