@@ -246,7 +246,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
         const_cast<int64_t*>(ps.ts)[j] = t;
         const_cast<int64_t*>(ps.n)[j] = nv;
         const_cast<uint32_t*>(ps.cfg)[j] = c;
-        const_cast<int64_t*>(ps.sms)[j] = sms;
+        if (ps.sms) const_cast<int64_t*>(ps.sms)[j] = sms;
         if (k0 >= win_base) continue;
         const CfgDev& C = cfgs[c];
         const double now = (double)t / 1e9;
@@ -259,9 +259,6 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
             pre.add[j] = key_alive(prev_when, sms, profile) ? (now - prev_last) * C.rate : __builtin_nan("");
         }
         pre.th[j] = fmin(C.limit_d, (double)nv);
-        pre.reset[j] = tb_reset_at(now, C);
-        pre.lq[j] = lua_tostring_roundtrip(now, profile);
-        pre.when[j] = expire_when(C.ttl_tb, sms);
     }
     __syncthreads();
     // segments: short ones replay serially, one thread each (exact fallbacks
@@ -314,17 +311,18 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
         }
         const uint8_t dec = ps.dec[j];
         const double tok = ps.tok[j];
-        int64_t rem, retry;
+        int64_t rem, retry, reset;
         if (k0 < win_base) {
-            tb_result(dec, tok, ps.n[j], cfgs[ps.cfg[j]], rem, retry);
+            tb_result_reset(dec, tok, ps.n[j], ps.ts[j], cfgs[ps.cfg[j]], rem, retry, reset);
         } else {
             rem = ps.rem[j];
             retry = ps.retry[j];
+            reset = ps.reset[j];
         }
         in.dec[i] = dec;
         in.rem[i] = rem;
         in.retry[i] = retry;
-        in.reset[i] = ps.reset[j];
+        in.reset[i] = reset;
         if (in.tok) in.tok[i] = tok;
     }
     if (ef) atomicOr(eflags, ef);
@@ -434,8 +432,7 @@ struct BatchSet {
     int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
     double* o_tok = nullptr;
     // token-bucket precomputation (k_permute)
-    double *q_add = nullptr, *q_th = nullptr, *q_lq = nullptr;
-    int64_t* q_when = nullptr;
+    double *q_add = nullptr, *q_th = nullptr;
     TbRuns runs{};                // the chain's committed runs (by start position)
     uint32_t* zero = nullptr;     // ctrl words + look-back status + huge claims (memset per batch)
     uint32_t* ctrl = nullptr;
@@ -485,10 +482,10 @@ struct rl_engine {
     // chain stream orders)
     uint32_t small_max = 0;
     int64_t *s_ts = nullptr, *s_n = nullptr, *s_sms = nullptr, *s_rem = nullptr, *s_retry = nullptr,
-            *s_reset = nullptr, *s_when = nullptr;
+            *s_reset = nullptr;
     uint32_t* s_cfg = nullptr;
     uint8_t* s_dec = nullptr;
-    double *s_tok = nullptr, *s_add = nullptr, *s_lq = nullptr, *s_th = nullptr;
+    double *s_tok = nullptr, *s_add = nullptr, *s_th = nullptr;
     hipEvent_t ev_small = nullptr;
     hipEvent_t ev_reset = nullptr;    // rl_reset_device: the DEL on `chain` -> the caller's stream
     int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
@@ -558,7 +555,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.rec);
     (void)hipFree(B.o_dec); (void)hipFree(B.o_rem); (void)hipFree(B.o_retry); (void)hipFree(B.o_reset);
     (void)hipFree(B.o_tok);
-    (void)hipFree(B.q_add); (void)hipFree(B.q_th); (void)hipFree(B.q_lq); (void)hipFree(B.q_when);
+    (void)hipFree(B.q_add); (void)hipFree(B.q_th);
     (void)hipFree(B.runs.len); (void)hipFree(B.runs.E); (void)hipFree(B.runs.D0); (void)hipFree(B.runs.D1);
     (void)hipFree(B.zero);
     (void)hipFree(B.kid);
@@ -592,8 +589,6 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     // reads them in aligned 128-element chunks that may end past the batch
     ok &= hipMalloc(&B.q_add, 8 * (M + 128)) == hipSuccess;
     ok &= hipMalloc(&B.q_th, 8 * (M + 128)) == hipSuccess;
-    ok &= hipMalloc(&B.q_lq, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&B.q_when, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.runs.len, 2 * M) == hipSuccess;
     ok &= hipMalloc(&B.runs.E, 2 * M) == hipSuccess;
     ok &= hipMalloc(&B.runs.D0, 8 * M) == hipSuccess;
@@ -631,8 +626,8 @@ static void free_all(rl_engine* e) {
     if (e->ev_small) (void)hipEventDestroy(e->ev_small);
     if (e->ev_reset) (void)hipEventDestroy(e->ev_reset);
     for (void* p : {(void*)e->s_ts, (void*)e->s_n, (void*)e->s_sms, (void*)e->s_rem, (void*)e->s_retry,
-                    (void*)e->s_reset, (void*)e->s_when, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
-                    (void*)e->s_add, (void*)e->s_lq, (void*)e->s_th})
+                    (void*)e->s_reset, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
+                    (void*)e->s_add, (void*)e->s_th})
         (void)hipFree(p);
     if (e->front) (void)hipStreamDestroy(e->front);
     if (e->chain) (void)hipStreamDestroy(e->chain);
@@ -727,10 +722,10 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_retry, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_tok, 8 * M) == hipSuccess;
-    for (int64_t** p : {&e->s_ts, &e->s_n, &e->s_sms, &e->s_rem, &e->s_retry, &e->s_reset, &e->s_when})
+    for (int64_t** p : {&e->s_ts, &e->s_n, &e->s_sms, &e->s_rem, &e->s_retry, &e->s_reset})
         ok &= hipMalloc(p, 8 * SMALL_MAX) == hipSuccess;
     // add / th: 128 elements of slack, as the batch sets' (exact_span reads ahead)
-    for (double** p : {&e->s_tok, &e->s_add, &e->s_lq, &e->s_th}) ok &= hipMalloc(p, 8 * (SMALL_MAX + 128)) == hipSuccess;
+    for (double** p : {&e->s_tok, &e->s_add, &e->s_th}) ok &= hipMalloc(p, 8 * (SMALL_MAX + 128)) == hipSuccess;
     ok &= hipMalloc(&e->s_cfg, 4 * SMALL_MAX) == hipSuccess;
     ok &= hipMalloc(&e->s_dec, SMALL_MAX) == hipSuccess;
     if (!ok) return bail(RL_ENOMEM);
@@ -855,8 +850,10 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         if (r != RL_OK) return r;
         a.key = e->small_kid;
     }
-    ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, e->s_sms, e->s_dec, e->s_rem, e->s_retry, e->s_reset, e->s_tok};
-    TbPre pre{e->s_add, e->s_th, e->s_reset, e->s_lq, e->s_when};
+    // sorted-order scratch; the server clock only when the caller gave one
+    ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, a.sms ? e->s_sms : nullptr, e->s_dec, e->s_rem, e->s_retry,
+               e->s_reset, e->s_tok};
+    TbPre pre{e->s_add, e->s_th};
     k_small<<<1, SMALL_BLOCK, 0, c>>>(m, a, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
                                       e->win_cap - 1, e->spill(), e->win_base, e->invalid_key, e->profile, ps, pre,
                                       std::max<uint32_t>(e->heavy_min, 32), e->d_eflags);
@@ -930,12 +927,12 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
                                       std::max(e->huge_min, e->heavy_min), lists);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
-    ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, B.p_sms, B.o_dec, B.o_rem, B.o_retry, B.o_reset, B.o_tok};
+    // (the server clock only when the caller gave one: else floor(ts / 1e6) where it is read)
+    ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, B.o_rem, B.o_retry, B.o_reset,
+               B.o_tok};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
     const int pgrid_r = (int)std::min<uint32_t>((m + 256 * PERM_R - 1) / (256 * PERM_R), (uint32_t)e->perm_grid);
-    // the TB reset time is state-independent: k_permute writes it straight
-    // into the sorted result buffer
-    TbPre pre{B.q_add, B.q_th, B.o_reset, B.q_lq, B.q_when};
+    TbPre pre{B.q_add, B.q_th};
     // front_done rides on k_permute's dispatch packet (no marker packet)
     // unless a stamp kernel follows it
     const bool bind_front = !sr;

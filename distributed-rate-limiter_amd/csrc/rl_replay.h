@@ -21,7 +21,7 @@ struct ReqArgs {
     const int64_t* ts;
     const int64_t* n;
     const uint32_t* cfg;
-    const int64_t* sms;   // nullable: server clock = floor(ts / 1e6)
+    const int64_t* sms;   // nullable: server clock = floor(ts / 1e6) (also in sorted order)
     uint8_t* dec;
     int64_t* rem;
     int64_t* retry;
@@ -31,7 +31,10 @@ struct ReqArgs {
 
 // State-independent token-bucket quantities of each request (sorted order),
 // computed in the permute pass: the previous request of the same key is the
-// previous sorted position (or, for a segment head, the table entry).
+// previous sorted position (or, for a segment head, the table entry).  The
+// rest of the script's state-free inputs are computed where they are used:
+// reset_at in the finish (tb_result_reset), last_refill and the TTL of a
+// segment's last request at its end (tb_store_end).
 struct TbPre {
     double* add;       // elapsed * refill_rate (tokenbucket.go:36-37); NaN when HMGET finds
                        // no live key (tokenbucket.go:31-34: tokens = capacity, add = 0).
@@ -39,14 +42,20 @@ struct TbPre {
                        // replay computes it (tb_head_add); k_permute fills the rest
     double* th;        // min(capacity, float64(n)): the script step allows or clamps
                        // exactly when capacity-free sum >= th (tokenbucket.go:38-43)
-    int64_t* reset;    // calculateResetTime (tokenbucket.go:161-165); aliases the sorted
-                       // result buffer, so TB replay never rewrites reset_at
-    double* lq;        // tostring(now) as stored in last_refill (tokenbucket.go:48)
-    int64_t* when;     // key expiry after this request's EXPIRE (tokenbucket.go:49)
 };
 
 __device__ inline int64_t req_server_ms(const ReqArgs& a, uint32_t i, int64_t t) {
     return a.sms ? a.sms[i] : floor_div(t, 1000000LL);
+}
+
+// the stored state after a token-bucket segment's last request j: HSET
+// last_refill = tostring(now) and the EXPIRE (tokenbucket.go:48-49)
+__device__ inline void tb_store_end(TbEntry* e, double tok, uint32_t j, const CfgDev* cfgs, int32_t profile,
+                                    const ReqArgs& a) {
+    const int64_t t = a.ts[j];
+    e->tok = tok;
+    e->last = lua_tostring_roundtrip((double)t / 1e9, profile);
+    e->when = expire_when(cfgs[a.cfg[j]].ttl_tb, req_server_ms(a, j, t));
 }
 
 __device__ inline void write_out(const ReqArgs& a, uint32_t i, const Out& o) {
@@ -58,9 +67,9 @@ __device__ inline void write_out(const ReqArgs& a, uint32_t i, const Out& o) {
 }
 
 // token bucket: replay writes the decision and the unquantized tokens only;
-// reset_at was written by k_permute (TbPre::reset) and remaining/retry_after
-// are functions of (decision, tokens, n, config) that k_unpermute evaluates
-// (tokenbucket.go:114-130, tb_result below)
+// remaining/retry_after/reset_at are functions of (decision, tokens, n, time,
+// config) that the finish evaluates (tokenbucket.go:114-130,161-165;
+// tb_result below)
 __device__ inline void write_out_tb(const ReqArgs& a, uint32_t i, uint8_t dec, double tokens) {
     a.dec[i] = dec;
     a.tok[i] = tokens;
@@ -92,7 +101,7 @@ __device__ inline Req load_req(const ReqArgs& a, uint32_t j) {
     r.t = a.ts[j];
     r.n = a.n[j];
     r.c = a.cfg[j];
-    r.sms = a.sms[j];
+    r.sms = req_server_ms(a, j, r.t);
     return r;
 }
 
@@ -129,7 +138,8 @@ __device__ inline double tb_head_add(const TbEntry* e, uint32_t j0, const CfgDev
                                      const ReqArgs& a) {
     const CfgDev& C = cfgs[a.cfg[j0]];
     const double now = (double)a.ts[j0] / 1e9;
-    return key_alive(e->when, a.sms[j0], profile) ? (now - e->last) * C.rate : __builtin_nan("");
+    return key_alive(e->when, req_server_ms(a, j0, a.ts[j0]), profile) ? (now - e->last) * C.rate
+                                                                          : __builtin_nan("");
 }
 
 __device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
@@ -142,9 +152,7 @@ __device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, co
         Out o = tb_chain_step(tok, alive, alive ? add : 0.0, a.n[j], 0, cfgs[a.cfg[j]], profile);
         write_out_tb(a, j, o.decision, o.tokens);
     }
-    e->tok = tok;
-    e->last = pre.lq[j1 - 1];
-    e->when = pre.when[j1 - 1];
+    tb_store_end(e, tok, j1 - 1, cfgs, profile, a);
 }
 
 // requests [j0, j1) of one window segment, one by one, from state w
@@ -577,7 +585,7 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
             const_cast<int64_t*>(out.ts)[j] = r[u].ts;
             const_cast<int64_t*>(out.n)[j] = r[u].n;
             const_cast<uint32_t*>(out.cfg)[j] = r[u].cfg;
-            const_cast<int64_t*>(out.sms)[j] = r[u].sms;
+            if (out.sms) const_cast<int64_t*>(out.sms)[j] = r[u].sms;   // only an explicit server clock
             if (k0[u] >= win_base) continue;
             const CfgDev& C = cfgs[r[u].cfg];
             const double now = (double)r[u].ts / 1e9;
@@ -590,9 +598,6 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
                                                                      : __builtin_nan("");
             }
             pre.th[j] = fmin(C.limit_d, (double)r[u].n);
-            pre.reset[j] = tb_reset_at(now, C);
-            pre.lq[j] = lua_tostring_roundtrip(now, profile);
-            pre.when[j] = expire_when(C.ttl_tb, r[u].sms);
         }
     }
 }
@@ -600,6 +605,14 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
 // Go's result arithmetic of a token-bucket step from the script's reply
 // (tokenbucket.go:114-130): Remaining = floor(tokens); RetryAfter from the
 // missing tokens when denied
+__device__ inline void tb_result(uint8_t dec, double tokens, int64_t n, const CfgDev& c, int64_t& rem,
+                                 int64_t& retry);
+// ... and ResetAt = calculateResetTime(now) (tokenbucket.go:161-165)
+__device__ inline void tb_result_reset(uint8_t dec, double tokens, int64_t n, int64_t ts, const CfgDev& c,
+                                       int64_t& rem, int64_t& retry, int64_t& reset) {
+    tb_result(dec, tokens, n, c, rem, retry);
+    reset = tb_reset_at((double)ts / 1e9, c);
+}
 __device__ inline void tb_result(uint8_t dec, double tokens, int64_t n, const CfgDev& c, int64_t& rem,
                                  int64_t& retry) {
     rem = go_f2i(floor(tokens));
@@ -630,17 +643,18 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
         }
         const uint8_t dec = sorted.dec[j];
         const double tok = sorted.tok[j];
-        int64_t rem, retry;
+        int64_t rem, retry, reset;
         if (k0 < win_base) {
-            tb_result(dec, tok, sorted.n[j], cfgs[sorted.cfg[j]], rem, retry);
+            tb_result_reset(dec, tok, sorted.n[j], sorted.ts[j], cfgs[sorted.cfg[j]], rem, retry, reset);
         } else {
             rem = sorted.rem[j];
             retry = sorted.retry[j];
+            reset = sorted.reset[j];
         }
         out.dec[i] = dec;
         out.rem[i] = rem;
         out.retry[i] = retry;
-        out.reset[i] = sorted.reset[j];
+        out.reset[i] = reset;
         if (out.tok) out.tok[i] = tok;
     }
 }
@@ -697,12 +711,12 @@ __global__ __launch_bounds__(256) void k_unpermute_bucket(const uint32_t* __rest
             r.dec = dec;
             r.tok = sorted.tok[j];
             if (k0 < win_base) {
-                tb_result(dec, r.tok, sorted.n[j], cfgs[sorted.cfg[j]], r.rem, r.retry);
+                tb_result_reset(dec, r.tok, sorted.n[j], sorted.ts[j], cfgs[sorted.cfg[j]], r.rem, r.retry, r.reset);
             } else {
                 r.rem = sorted.rem[j];
                 r.retry = sorted.retry[j];
+                r.reset = sorted.reset[j];
             }
-            r.reset = sorted.reset[j];
         }
         rec[q] = r;
         at[q] = atomicAdd(&s_cnt[i >> UP_BUCKET_BITS], 1u);

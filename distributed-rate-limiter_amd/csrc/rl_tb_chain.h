@@ -1000,11 +1000,7 @@ __device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, u
         E = __builtin_amdgcn_readfirstlane(so.E);
         mode = __builtin_amdgcn_readfirstlane(so.mode);
     }
-    if ((threadIdx.x & 63) == 0) {
-        e->tok = tb_value(D, E, profile);
-        e->last = pre.lq[j1 - 1];
-        e->when = pre.when[j1 - 1];
-    }
+    if ((threadIdx.x & 63) == 0) tb_store_end(e, tb_value(D, E, profile), j1 - 1, cfgs, profile, a);
 }
 
 // Replay one heavy fixed / sliding window segment [j0, j1) with ONE wave.
@@ -1072,7 +1068,7 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
                 const bool v = j < j1;
                 t[q] = v ? a.ts[j] : 0;
                 n[q] = v ? a.n[j] : 0;
-                sm[q] = v ? a.sms[j] : 0;
+                sm[q] = v ? req_server_ms(a, j, t[q]) : 0;
                 // window_start(t) == ws without two 64-bit divisions: W >= 1 s
                 // here (ttl_c > 0), so windows whose starts differ also differ
                 // in the key's second, and t is in r0's window iff it lies in
@@ -1350,9 +1346,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
 #endif
     if (tid == 0) {
         const ChState s = sh.st[par];
-        e->tok = tb_value(s.D, s.E, profile);
-        e->last = pre.lq[j1 - 1];
-        e->when = pre.when[j1 - 1];
+        tb_store_end(e, tb_value(s.D, s.E, profile), j1 - 1, cfgs, profile, a);
         if (dbg) {
             atomicAdd(&dbg[0], nrounds);
             atomicAdd(&dbg[1], iters);
