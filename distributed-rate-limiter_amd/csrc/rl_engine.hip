@@ -120,12 +120,12 @@ __device__ inline uint32_t probe_request(uint64_t k, uint32_t c, int64_t nn, con
 // (inputs, then every first table probe) before resolving any: the kernel is
 // latency-bound on random table reads, and this keeps PROBE_R of them in
 // flight per thread instead of one.
-template <int PROBE_R>
+template <int PROBE_R, bool XS>
 __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     uint32_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ n,
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
     uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
-    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, ReqArgs a, ReqRec* __restrict__ rec,
+    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, ReqArgs a, ReqRec<XS>* __restrict__ rec,
     uint32_t* eflags) {
     __shared__ uint32_t lh[4][RADIX];
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             c[r] = v ? cfg[i] : 0u;
             nn[r] = v ? n[i] : 0;
             t[r] = v ? a.ts[i] : 0;
-            sms[r] = v && a.sms ? a.sms[i] : 0;
+            sms[r] = v && XS ? a.sms[i] : 0;
         }
 #pragma unroll
         for (int r = 0; r < PROBE_R; r++) {   // first probes, all in flight
@@ -168,15 +168,9 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
                 else slot = tbk[r] ? s : win_base + s;
             }
             sk[i] = slot;
-            // one 32-B record per request: k_permute's sorted-order gather then
+            // one record per request: k_permute's sorted-order gather then
             // touches one line fragment instead of four arrays
-            ReqRec q;
-            q.ts = t[r];
-            q.n = nn[r];
-            q.sms = a.sms ? sms[r] : floor_div(t[r], 1000000LL);
-            q.cfg = c[r];
-            q.pad = 0;
-            rec[i] = q;
+            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r]);
             for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
         }
     }
@@ -310,15 +304,9 @@ __global__ __launch_bounds__(SMALL_BLOCK) void k_small(
             continue;
         }
         const uint8_t dec = ps.dec[j];
-        const double tok = ps.tok[j];
         int64_t rem, retry, reset;
-        if (k0 < win_base) {
-            tb_result_reset(dec, tok, ps.n[j], ps.ts[j], cfgs[ps.cfg[j]], rem, retry, reset);
-        } else {
-            rem = ps.rem[j];
-            retry = ps.retry[j];
-            reset = ps.reset[j];
-        }
+        double tok;
+        finish_result(dec, ps.tok[j], ps.ts[j], ps.n[j], cfgs[ps.cfg[j]], rem, retry, reset, tok);
         in.dec[i] = dec;
         in.rem[i] = rem;
         in.retry[i] = retry;
@@ -387,7 +375,8 @@ namespace {
 
 constexpr int NSTAGES = 5;
 constexpr uint32_t STAMP_RING = 256;
-constexpr int NSETS = 3;          // batch buffer sets: grouping b+1 | replay b | finish b-1
+constexpr int NSETS = 4;          // batch buffer sets: grouping b+2, b+1 | replay b | finish b-1
+constexpr int NFRONTS = 2;        // grouping streams (consecutive batches alternate)
 constexpr int GROUP_LDS = 4096;   // LDS floor of the grouping / finish kernels (see rl_engine::chain_pad)
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
@@ -427,10 +416,9 @@ struct BatchSet {
     // requests and results in sorted order (k_permute / k_unpermute)
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
-    ReqRec* rec = nullptr;        // requests packed in arrival order (k_probe -> k_permute)
+    void* rec = nullptr;          // requests packed in arrival order (k_probe -> k_permute): ReqRec<XS>
     uint8_t* o_dec = nullptr;
-    int64_t *o_rem = nullptr, *o_retry = nullptr, *o_reset = nullptr;
-    double* o_tok = nullptr;
+    double* o_tok = nullptr;      // tokens (token bucket) / Remaining bits (window): finish_result
     // token-bucket precomputation (k_permute)
     double *q_add = nullptr, *q_th = nullptr;
     TbRuns runs{};                // the chain's committed runs (by start position)
@@ -453,7 +441,8 @@ struct rl_engine {
     // hardware queue each at HIP's default of four queues per process (streams
     // sharing a queue would serialize the replay and the finish)
     hipStream_t stream = nullptr;
-    hipStream_t front = nullptr;      // grouping
+    hipStream_t front[NFRONTS] = {};  // grouping, batch b on front[b mod nfronts]
+    int nfronts = NFRONTS, next_front = 0;
     hipStream_t chain = nullptr;      // replays, in batch order
     hipStream_t tail = nullptr;       // finishes
     hipEvent_t ev_in = nullptr;       // inputs ready (non-pipelined device API, host API)
@@ -481,8 +470,7 @@ struct rl_engine {
     // sorted-order scratch (reused by consecutive small batches, which the
     // chain stream orders)
     uint32_t small_max = 0;
-    int64_t *s_ts = nullptr, *s_n = nullptr, *s_sms = nullptr, *s_rem = nullptr, *s_retry = nullptr,
-            *s_reset = nullptr;
+    int64_t *s_ts = nullptr, *s_n = nullptr, *s_sms = nullptr;
     uint32_t* s_cfg = nullptr;
     uint8_t* s_dec = nullptr;
     double *s_tok = nullptr, *s_add = nullptr, *s_th = nullptr;
@@ -553,7 +541,7 @@ static void free_set(BatchSet& B) {
     for (auto* l : B.list) (void)hipFree(l);
     (void)hipFree(B.p_ts); (void)hipFree(B.p_n); (void)hipFree(B.p_sms); (void)hipFree(B.p_cfg);
     (void)hipFree(B.rec);
-    (void)hipFree(B.o_dec); (void)hipFree(B.o_rem); (void)hipFree(B.o_retry); (void)hipFree(B.o_reset);
+    (void)hipFree(B.o_dec);
     (void)hipFree(B.o_tok);
     (void)hipFree(B.q_add); (void)hipFree(B.q_th);
     (void)hipFree(B.runs.len); (void)hipFree(B.runs.E); (void)hipFree(B.runs.D0); (void)hipFree(B.runs.D1);
@@ -579,11 +567,8 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_n, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&B.rec, sizeof(ReqRec) * M) == hipSuccess;
+    ok &= hipMalloc(&B.rec, sizeof(ReqRec<true>) * M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
-    ok &= hipMalloc(&B.o_rem, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&B.o_retry, 8 * M) == hipSuccess;
-    ok &= hipMalloc(&B.o_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.o_tok, 8 * M) == hipSuccess;
     // q_add and q_th carry 128 elements of slack: the chain's loader wave
     // reads them in aligned 128-element chunks that may end past the batch
@@ -625,11 +610,11 @@ static void free_all(rl_engine* e) {
     if (e->ev_in) (void)hipEventDestroy(e->ev_in);
     if (e->ev_small) (void)hipEventDestroy(e->ev_small);
     if (e->ev_reset) (void)hipEventDestroy(e->ev_reset);
-    for (void* p : {(void*)e->s_ts, (void*)e->s_n, (void*)e->s_sms, (void*)e->s_rem, (void*)e->s_retry,
-                    (void*)e->s_reset, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
+    for (void* p : {(void*)e->s_ts, (void*)e->s_n, (void*)e->s_sms, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
                     (void*)e->s_add, (void*)e->s_th})
         (void)hipFree(p);
-    if (e->front) (void)hipStreamDestroy(e->front);
+    for (auto f : e->front)
+        if (f) (void)hipStreamDestroy(f);
     if (e->chain) (void)hipStreamDestroy(e->chain);
     if (e->tail) (void)hipStreamDestroy(e->tail);
 }
@@ -637,7 +622,8 @@ static void free_all(rl_engine* e) {
 // every queued kernel of the engine has finished (the engine's streams and,
 // through the back_done events, any caller stream a batch was enqueued on)
 static int drain(rl_engine* e) {
-    HIPCHK(e, hipStreamSynchronize(e->front));
+    for (auto f : e->front)
+        if (f) HIPCHK(e, hipStreamSynchronize(f));
     HIPCHK(e, hipStreamSynchronize(e->chain));
     HIPCHK(e, hipStreamSynchronize(e->tail));
     for (auto& B : e->set)
@@ -685,8 +671,11 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int c = 0; c < ncu; c++)
             if (c % 32 != 31 || ncu < 64) mask[c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(&e->front, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
-            hipExtStreamCreateWithCUMask(&e->tail, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+        if (const char* v = getenv("RL_FRONTS")) e->nfronts = std::max(1, std::min(NFRONTS, atoi(v)));
+        for (int k = 0; k < e->nfronts; k++)
+            if (hipExtStreamCreateWithCUMask(&e->front[k], (uint32_t)mask.size(), mask.data()) != hipSuccess)
+                return bail(RL_EDEVICE);
+        if (hipExtStreamCreateWithCUMask(&e->tail, (uint32_t)mask.size(), mask.data()) != hipSuccess)
             return bail(RL_EDEVICE);
     }
     {
@@ -722,7 +711,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_retry, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_reset, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_tok, 8 * M) == hipSuccess;
-    for (int64_t** p : {&e->s_ts, &e->s_n, &e->s_sms, &e->s_rem, &e->s_retry, &e->s_reset})
+    for (int64_t** p : {&e->s_ts, &e->s_n, &e->s_sms})
         ok &= hipMalloc(p, 8 * SMALL_MAX) == hipSuccess;
     // add / th: 128 elements of slack, as the batch sets' (exact_span reads ahead)
     for (double** p : {&e->s_tok, &e->s_add, &e->s_th}) ok &= hipMalloc(p, 8 * (SMALL_MAX + 128)) == hipSuccess;
@@ -851,8 +840,8 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         a.key = e->small_kid;
     }
     // sorted-order scratch; the server clock only when the caller gave one
-    ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, a.sms ? e->s_sms : nullptr, e->s_dec, e->s_rem, e->s_retry,
-               e->s_reset, e->s_tok};
+    ReqArgs ps{nullptr, e->s_ts, e->s_n, e->s_cfg, a.sms ? e->s_sms : nullptr, e->s_dec, nullptr, nullptr,
+               nullptr, e->s_tok};
     TbPre pre{e->s_add, e->s_th};
     k_small<<<1, SMALL_BLOCK, 0, c>>>(m, a, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
                                       e->win_cap - 1, e->spill(), e->win_base, e->invalid_key, e->profile, ps, pre,
@@ -872,7 +861,12 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     BatchSet& B = e->set[e->next_set];
     e->last_set = e->next_set;
     e->next_set = (e->next_set + 1) % NSETS;
-    hipStream_t f = e->front;
+    // consecutive batches group on alternating streams: the grouping kernels
+    // are latency-bound (random table probes, look-back sort passes of a few
+    // hundred blocks), so two batches' groupings overlap on the CUs the
+    // replay leaves free
+    hipStream_t f = e->front[e->next_front];
+    e->next_front = (e->next_front + 1) % e->nfronts;
     if (!inputs_ready) {
         HIPCHK(e, hipEventRecord(e->ev_in, s));
         HIPCHK(e, hipStreamWaitEvent(f, e->ev_in, 0));
@@ -901,10 +895,17 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // few enough blocks that the per-block histogram flush (3 x 256 global
     // atomics per block on 768 shared words) stays cheap
     const int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, (uint32_t)e->probe_grid);
-    k_probe<1><<<probe_grid, PROBE_BLOCK, 0, f>>>(m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(),
-                                                       e->d_tb, e->tb_cap - 1, e->d_win, e->win_cap - 1,
-                                                       e->win_base, e->invalid_key, B.sk0, ghist,
-                                                       e->sort_passes, a, B.rec, e->d_eflags);
+    const bool xs = a.sms != nullptr;   // explicit server clock: 32-byte request records
+    if (xs)
+        k_probe<1, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
+            m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, a,
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags);
+    else
+        k_probe<1, false><<<probe_grid, PROBE_BLOCK, 0, f>>>(
+            m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, a,
+            static_cast<ReqRec<false>*>(B.rec), e->d_eflags);
     if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
@@ -928,17 +929,22 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
                                       std::max(e->huge_min, e->heavy_min), lists);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     // (the server clock only when the caller gave one: else floor(ts / 1e6) where it is read)
-    ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, B.o_rem, B.o_retry, B.o_reset,
+    ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, nullptr, nullptr, nullptr,
                B.o_tok};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
-    const int pgrid_r = (int)std::min<uint32_t>((m + 256 * PERM_R - 1) / (256 * PERM_R), (uint32_t)e->perm_grid);
+    const int pgrid_r = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
     TbPre pre{B.q_add, B.q_th};
     // front_done rides on k_permute's dispatch packet (no marker packet)
     // unless a stamp kernel follows it
     const bool bind_front = !sr;
-    hipExtLaunchKernelGGL(k_permute, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
-                          bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base, e->d_cfg,
-                          e->profile, B.rec, ps, pre);
+    if (xs)
+        hipExtLaunchKernelGGL(k_permute<true>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
+                              bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
+                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre);
+    else
+        hipExtLaunchKernelGGL(k_permute<false>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
+                              bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
+                              e->d_cfg, e->profile, static_cast<const ReqRec<false>*>(B.rec), a.n, ps, pre);
     if (tall) (void)hipEventRecord(ev[3], f);
     if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 1);
     if (!bind_front) HIPCHK(e, hipEventRecord(B.front_done, f));
@@ -991,10 +997,10 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         // results to the caller's order through arrival-index buckets: no
         // scattered partial-line stores
         k_unpermute_bucket<<<(m + 256 * UP_ITEMS - 1) / (256 * UP_ITEMS), 256, GROUP_LDS, t>>>(
-            kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, B.upb, B.ctrl + CTRL_UPB);
-        k_unpermute_bucket_out<<<(m + UP_BUCKET - 1) / UP_BUCKET, 256, 0, t>>>(m, B.upb, a);
+            kin, vin, m, e->invalid_key, ps, B.upb, B.ctrl + CTRL_UPB);
+        k_unpermute_bucket_out<<<(m + UP_BUCKET - 1) / UP_BUCKET, 256, 0, t>>>(m, B.upb, e->d_cfg, a);
     } else {
-        k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->win_base, e->d_cfg, ps, a);
+        k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->d_cfg, ps, a);
     }
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 5);
     if (e->timing) {
@@ -1022,8 +1028,15 @@ static int warm_up(rl_engine* e) {
     HIPCHK(e, hipMemsetAsync(e->d_ts, 0, 8 * (size_t)mb, s));
     HIPCHK(e, hipMemsetAsync(e->d_cfgid, 0, 4 * (size_t)mb, s));
     ReqArgs a{e->d_key, e->d_ts, e->d_n, e->d_cfgid, nullptr, e->d_dec, e->d_rem, e->d_retry, e->d_reset, e->d_tok};
+    HIPCHK(e, hipMemsetAsync(e->d_sms, 0, 8 * (size_t)mb, s));
     for (uint32_t m : {1u, mb}) {
         const int r = run_batch(e, m, a, s, false);
+        if (r != RL_OK) return r;
+    }
+    {   // the record layout with an explicit server clock (k_probe / k_permute <true>)
+        ReqArgs ax = a;
+        ax.sms = e->d_sms;
+        const int r = run_batch(e, mb, ax, s, false);
         if (r != RL_OK) return r;
     }
     const int r = drain(e);

@@ -58,12 +58,12 @@ __device__ inline void tb_store_end(TbEntry* e, double tok, uint32_t j, const Cf
     e->when = expire_when(cfgs[a.cfg[j]].ttl_tb, req_server_ms(a, j, t));
 }
 
+// window counters: the replay writes the decision and Remaining only (in the
+// value slot, as int64 bits); reset_at and retry_after are functions of the
+// request's time and config that the finish evaluates (finish_result)
 __device__ inline void write_out(const ReqArgs& a, uint32_t i, const Out& o) {
     a.dec[i] = o.decision;
-    a.rem[i] = o.remaining;
-    a.retry[i] = o.retry;
-    a.reset[i] = o.reset_at;
-    if (a.tok) a.tok[i] = o.tokens;
+    a.tok[i] = __longlong_as_double(o.remaining);
 }
 
 // token bucket: replay writes the decision and the unquantized tokens only;
@@ -516,89 +516,112 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
     }
 }
 
-// requests in sorted order (one coalesced pass; random reads of the 28 B
-// request records, which stay in the Infinity Cache at 1M-request batches),
-// plus the token-bucket precomputation (TbPre)
-// One request as k_probe packs it in arrival order (server clock resolved):
-// the sorted-order gather of k_permute reads one 32-B record per request
-// instead of four scattered array elements.
-struct alignas(32) ReqRec {
+// One request as k_probe packs it in arrival order: the sorted-order gather
+// of k_permute reads one record per request instead of four scattered array
+// elements.  Without an explicit server clock (XS false, the common case) the
+// record is 16 bytes -- time, config and n when it fits 32 bits (a larger n
+// is read from the caller's array) -- and the clock is floor(ts / 1e6); with
+// one (XS, the routed path's store clock) it is 32 bytes.
+template <bool XS> struct ReqRec;
+template <> struct alignas(16) ReqRec<false> {
+    int64_t ts;
+    uint32_t cfg, n32;
+};
+template <> struct alignas(32) ReqRec<true> {
     int64_t ts, n, sms;
     uint32_t cfg, pad;
 };
+constexpr uint32_t REC_N_WIDE = 0xffffffffu;   // n32: n does not fit (read the caller's n)
+static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 32, "request records");
+
+template <bool XS>
+__device__ inline ReqRec<XS> rec_pack(int64_t t, int64_t n, int64_t sms, uint32_t c) {
+    if constexpr (XS) {
+        return ReqRec<true>{t, n, sms, c, 0u};
+    } else {
+        (void)sms;
+        return ReqRec<false>{t, c, (n > 0 && n < (int64_t)REC_N_WIDE) ? (uint32_t)n : REC_N_WIDE};
+    }
+}
+template <bool XS>
+__device__ inline int64_t rec_n(const ReqRec<XS>& r, const int64_t* __restrict__ n_in, uint32_t i) {
+    if constexpr (XS) {
+        (void)n_in; (void)i;
+        return r.n;
+    } else {
+        return r.n32 != REC_N_WIDE ? (int64_t)r.n32 : n_in[i];
+    }
+}
+template <bool XS>
+__device__ inline int64_t rec_sms(const ReqRec<XS>& r) {
+    if constexpr (XS) return r.sms;
+    else return floor_div(r.ts, 1000000LL);
+}
 
 // requests to sorted order + the state-free token-bucket precomputation.
-// Each wave covers 64 consecutive sorted positions per chunk and PERM_R chunks
-// at once (their sorted-key / index loads, then their record gathers, all in
-// flight before any use: the kernel waits on random gathers); a request's
-// predecessor in its segment (position j-1) is the neighbouring lane's
-// record, so only lane 0 gathers a second one.
-constexpr int PERM_R = 1;   // 4 measured no faster (the gathers are not per-thread latency bound)
+// Each wave covers 64 consecutive sorted positions; a request's predecessor
+// in its segment (position j-1) is the neighbouring lane's record, so only
+// lane 0 gathers a second one.  n_in: the caller's n (arrival order), for a
+// record whose n did not fit.
+template <bool XS>
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
                                                  const CfgDev* __restrict__ cfgs, int32_t profile,
-                                                 const ReqRec* __restrict__ rec, ReqArgs out, TbPre pre) {
+                                                 const ReqRec<XS>* __restrict__ rec, const int64_t* __restrict__ n_in,
+                                                 ReqArgs out, TbPre pre) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t stride = gridDim.x * blockDim.x * PERM_R;
-    for (uint32_t base = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * PERM_R; base < m; base += stride) {
-        uint32_t k0[PERM_R], kpl[PERM_R], ix[PERM_R], ixp[PERM_R];
-        ReqRec r[PERM_R], q[PERM_R];
-#pragma unroll
-        for (int u = 0; u < PERM_R; u++) {
-            const uint32_t j = base + u * 64 + lane;
-            k0[u] = j < m ? sk[j] : invalid_key;
-            ix[u] = k0[u] != invalid_key ? sv[j] : 0u;
-            // lane 0: the predecessor at j-1 (a previous chunk's last lane)
-            kpl[u] = invalid_key;
-            ixp[u] = 0u;
-            if (lane == 0 && j > 0 && k0[u] != invalid_key && k0[u] < win_base) {
-                kpl[u] = sk[j - 1];
-                if (kpl[u] == k0[u]) ixp[u] = sv[j - 1];
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < m; base += stride) {
+        const uint32_t j = base + lane;
+        const uint32_t k0 = j < m ? sk[j] : invalid_key;
+        const uint32_t ix = k0 != invalid_key ? sv[j] : 0u;
+        // lane 0: the predecessor at j-1 (a previous chunk's last lane)
+        uint32_t kpl = invalid_key, ixp = 0u;
+        if (lane == 0 && j > 0 && k0 != invalid_key && k0 < win_base) {
+            kpl = sk[j - 1];
+            if (kpl == k0) ixp = sv[j - 1];
+        }
+        ReqRec<XS> r{}, q{};
+        if (k0 != invalid_key) r = rec[ix];
+        if (lane == 0 && kpl == k0 && k0 != invalid_key) q = rec[ixp];
+        const bool valid = k0 != invalid_key;
+        const int64_t sms = rec_sms<XS>(r);
+        // predecessor (j-1) fields from the lane below
+        uint32_t kp = __shfl_up(k0, 1);
+        int64_t tp = __shfl_up(r.ts, 1);
+        int64_t smsp = __shfl_up(sms, 1);
+        uint32_t cp = __shfl_up(r.cfg, 1);
+        if (lane == 0) {
+            kp = invalid_key;
+            if (kpl == k0 && valid) {
+                kp = k0;
+                tp = q.ts;
+                smsp = rec_sms<XS>(q);
+                cp = q.cfg;
             }
         }
-#pragma unroll
-        for (int u = 0; u < PERM_R; u++) {
-            r[u] = ReqRec{};
-            if (k0[u] != invalid_key) r[u] = rec[ix[u]];
-            if (lane == 0 && kpl[u] == k0[u] && k0[u] != invalid_key) q[u] = rec[ixp[u]];
+        if (!valid) continue;
+        const int64_t nn = rec_n<XS>(r, n_in, ix);
+        // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
+        const_cast<int64_t*>(out.ts)[j] = r.ts;
+        const_cast<int64_t*>(out.n)[j] = nn;
+        const_cast<uint32_t*>(out.cfg)[j] = r.cfg;
+        if (XS) const_cast<int64_t*>(out.sms)[j] = sms;   // only an explicit server clock
+        if (k0 >= win_base) continue;
+        const CfgDev& C = cfgs[r.cfg];
+        const double now = (double)r.ts / 1e9;
+        // state-free: a head's add needs the table (tb_head_add, at replay)
+        // and the table is still being updated by the previous batch; a
+        // placeholder keeps the stores full lines (the replay writes the
+        // head's own add where it is read)
+        double add = __builtin_nan("");
+        if (kp == k0) {
+            const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
+            const int64_t prev_when = expire_when(cfgs[cp].ttl_tb, smsp);
+            if (key_alive(prev_when, sms, profile)) add = (now - prev_last) * C.rate;
         }
-#pragma unroll
-        for (int u = 0; u < PERM_R; u++) {
-            const uint32_t j = base + u * 64 + lane;
-            const bool valid = k0[u] != invalid_key;
-            // predecessor (j-1) fields from the lane below
-            uint32_t kp = __shfl_up(k0[u], 1);
-            int64_t tp = __shfl_up(r[u].ts, 1);
-            int64_t smsp = __shfl_up(r[u].sms, 1);
-            uint32_t cp = __shfl_up(r[u].cfg, 1);
-            if (lane == 0) {
-                kp = invalid_key;
-                if (kpl[u] == k0[u] && valid) {
-                    kp = k0[u];
-                    tp = q[u].ts;
-                    smsp = q[u].sms;
-                    cp = q[u].cfg;
-                }
-            }
-            if (!valid) continue;
-            // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
-            const_cast<int64_t*>(out.ts)[j] = r[u].ts;
-            const_cast<int64_t*>(out.n)[j] = r[u].n;
-            const_cast<uint32_t*>(out.cfg)[j] = r[u].cfg;
-            if (out.sms) const_cast<int64_t*>(out.sms)[j] = r[u].sms;   // only an explicit server clock
-            if (k0[u] >= win_base) continue;
-            const CfgDev& C = cfgs[r[u].cfg];
-            const double now = (double)r[u].ts / 1e9;
-            // state-free: a head's add needs the table (tb_head_add, at replay)
-            // and the table is still being updated by the previous batch
-            if (kp == k0[u]) {
-                const double prev_last = lua_tostring_roundtrip((double)tp / 1e9, profile);
-                const int64_t prev_when = expire_when(cfgs[cp].ttl_tb, smsp);
-                pre.add[j] = key_alive(prev_when, r[u].sms, profile) ? (now - prev_last) * C.rate
-                                                                     : __builtin_nan("");
-            }
-            pre.th[j] = fmin(C.limit_d, (double)r[u].n);
-        }
+        pre.add[j] = add;
+        pre.th[j] = fmin(C.limit_d, (double)nn);
     }
 }
 
@@ -625,31 +648,38 @@ __device__ inline void tb_result(uint8_t dec, double tokens, int64_t n, const Cf
     }
 }
 
-// results from sorted order back to the caller's order (token-bucket
-// remaining/retry_after are finished here, off the replay's critical path)
+// The Result fields of one executed request from the replay's compact output
+// -- the decision and one value: the Lua `tokens` of a token bucket, Remaining
+// of a window counter -- and the request itself: token bucket
+// tokenbucket.go:114-130 (remaining, retry) and :161-165 (reset_at); window
+// counters fixedwindow.go:101-114 / slidingwindow.go:108-121 (reset_at =
+// window start + W, retry = time to it when denied; 0 on a script error)
+__device__ inline void finish_result(uint8_t dec, double val, int64_t t, int64_t n, const CfgDev& c, int64_t& rem,
+                                     int64_t& retry, int64_t& reset, double& tok) {
+    if (c.alg == ALG_TOKEN_BUCKET) {
+        tb_result_reset(dec, val, n, t, c, rem, retry, reset);
+        tok = val;
+        return;
+    }
+    rem = __double_as_longlong(val);
+    reset = wadd(wmul(window_start(t, c), NS_PER_S), c.window);
+    retry = dec == DEC_DENIED ? until_reset(reset, t) : 0;
+    tok = 0.0;
+}
+
+// results from sorted order back to the caller's order (batches above UP_MAX)
 __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
-                                                   uint32_t m, uint32_t invalid_key, uint32_t win_base,
-                                                   const CfgDev* __restrict__ cfgs, ReqArgs sorted, ReqArgs out) {
+                                                   uint32_t m, uint32_t invalid_key, const CfgDev* __restrict__ cfgs,
+                                                   ReqArgs sorted, ReqArgs out) {
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
         const uint32_t k0 = sk[j];
         const uint32_t i = sv[j];
-        if (k0 == invalid_key) {   // rejected by k_probe (n <= 0, unknown config or key, table full)
-            out.dec[i] = DEC_INVALID;
-            out.rem[i] = 0;
-            out.retry[i] = 0;
-            out.reset[i] = 0;
-            if (out.tok) out.tok[i] = 0.0;
-            continue;
-        }
-        const uint8_t dec = sorted.dec[j];
-        const double tok = sorted.tok[j];
-        int64_t rem, retry, reset;
-        if (k0 < win_base) {
-            tb_result_reset(dec, tok, sorted.n[j], sorted.ts[j], cfgs[sorted.cfg[j]], rem, retry, reset);
-        } else {
-            rem = sorted.rem[j];
-            retry = sorted.retry[j];
-            reset = sorted.reset[j];
+        uint8_t dec = DEC_INVALID;   // rejected by k_probe (n <= 0, unknown config or key, table full)
+        int64_t rem = 0, retry = 0, reset = 0;
+        double tok = 0.0;
+        if (k0 != invalid_key) {
+            dec = sorted.dec[j];
+            finish_result(dec, sorted.tok[j], sorted.ts[j], sorted.n[j], cfgs[sorted.cfg[j]], rem, retry, reset, tok);
         }
         out.dec[i] = dec;
         out.rem[i] = rem;
@@ -659,32 +689,31 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
     }
 }
 
-// Results to the caller's order without scattered stores (m <= UP_MAX).
-// k_unpermute writes five arrays at random arrival indices: every store is a
-// partial line.  Here (1) k_unpermute_bucket reads the results in sorted
-// order and writes one 40-byte record per request into the bucket of its
-// arrival index (UP_BUCKET consecutive indices; every bucket is full, so
-// bucket b starts at b * UP_BUCKET and a block-aggregated atomic per bucket
-// hands out positions inside it), then (2) k_unpermute_bucket_out places one
-// bucket's records in LDS by arrival index and writes every output array with
-// full-line, coalesced stores.
+// Results to the caller's order without scattered stores (m <= UP_MAX), in
+// two coalesced passes: (1) k_unpermute_bucket reads the replay's compact
+// results in sorted order (decision + value) and writes one 16-byte record per
+// request into the bucket of its arrival index (UP_BUCKET consecutive
+// indices; every bucket is full, so bucket b starts at b * UP_BUCKET and a
+// block-aggregated atomic per bucket hands out positions inside it); (2)
+// k_unpermute_bucket_out places one bucket's records in LDS by arrival index
+// and, reading each request's time, n and config in arrival order (the
+// caller's inputs, coalesced), finishes the Result fields (finish_result) and
+// writes every output array with full-line stores.
 constexpr int UP_BUCKET_BITS = 11;
 constexpr uint32_t UP_BUCKET = 1u << UP_BUCKET_BITS;   // arrival indices per bucket
 constexpr uint32_t UP_MAX = 1u << 20;                  // batches up to 2^20: <= 512 buckets
 constexpr uint32_t UP_NB = UP_MAX / UP_BUCKET;
 constexpr int UP_ITEMS = 8;                            // sorted positions per thread (k_unpermute_bucket)
 
-struct alignas(8) UpRec {
+struct alignas(16) UpRec {
     uint32_t i;        // arrival index
     uint32_t dec;
-    int64_t rem, retry, reset;
-    double tok;
+    double val;        // tokens (token bucket) / Remaining bits (window)
 };
 
 __global__ __launch_bounds__(256) void k_unpermute_bucket(const uint32_t* __restrict__ sk,
                                                           const uint32_t* __restrict__ sv, uint32_t m,
-                                                          uint32_t invalid_key, uint32_t win_base,
-                                                          const CfgDev* __restrict__ cfgs, ReqArgs sorted,
+                                                          uint32_t invalid_key, ReqArgs sorted,
                                                           UpRec* __restrict__ bucketed, uint32_t* bucket_ctr) {
     __shared__ uint32_t s_cnt[UP_NB], s_base[UP_NB];
     const uint32_t nb = (m + UP_BUCKET - 1) >> UP_BUCKET_BITS;
@@ -698,28 +727,9 @@ __global__ __launch_bounds__(256) void k_unpermute_bucket(const uint32_t* __rest
         const uint32_t j = j0 + q * 256 + threadIdx.x;
         at[q] = 0xffffffffu;
         if (j >= m) continue;
-        const uint32_t k0 = sk[j];
-        const uint32_t i = sv[j];
-        UpRec r;
-        r.i = i;
-        if (k0 == invalid_key) {   // rejected by k_probe (n <= 0, unknown config or key, table full)
-            r.dec = DEC_INVALID;
-            r.rem = r.retry = r.reset = 0;
-            r.tok = 0.0;
-        } else {
-            const uint8_t dec = sorted.dec[j];
-            r.dec = dec;
-            r.tok = sorted.tok[j];
-            if (k0 < win_base) {
-                tb_result_reset(dec, r.tok, sorted.n[j], sorted.ts[j], cfgs[sorted.cfg[j]], r.rem, r.retry, r.reset);
-            } else {
-                r.rem = sorted.rem[j];
-                r.retry = sorted.retry[j];
-                r.reset = sorted.reset[j];
-            }
-        }
-        rec[q] = r;
-        at[q] = atomicAdd(&s_cnt[i >> UP_BUCKET_BITS], 1u);
+        const bool ok = sk[j] != invalid_key;   // else rejected by k_probe
+        rec[q] = UpRec{sv[j], ok ? (uint32_t)sorted.dec[j] : (uint32_t)DEC_INVALID, ok ? sorted.tok[j] : 0.0};
+        at[q] = atomicAdd(&s_cnt[rec[q].i >> UP_BUCKET_BITS], 1u);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += 256)
@@ -734,9 +744,8 @@ __global__ __launch_bounds__(256) void k_unpermute_bucket(const uint32_t* __rest
 }
 
 __global__ __launch_bounds__(256) void k_unpermute_bucket_out(uint32_t m, const UpRec* __restrict__ bucketed,
-                                                              ReqArgs out) {
-    __shared__ int64_t s_rem[UP_BUCKET], s_retry[UP_BUCKET], s_reset[UP_BUCKET];
-    __shared__ double s_tok[UP_BUCKET];
+                                                              const CfgDev* __restrict__ cfgs, ReqArgs out) {
+    __shared__ double s_val[UP_BUCKET];
     __shared__ uint8_t s_dec[UP_BUCKET];
     const uint32_t b = blockIdx.x;
     const uint32_t base = b * UP_BUCKET;
@@ -745,18 +754,21 @@ __global__ __launch_bounds__(256) void k_unpermute_bucket_out(uint32_t m, const 
         const UpRec r = bucketed[(size_t)base + k];
         const uint32_t o = r.i - base;
         s_dec[o] = (uint8_t)r.dec;
-        s_rem[o] = r.rem;
-        s_retry[o] = r.retry;
-        s_reset[o] = r.reset;
-        s_tok[o] = r.tok;
+        s_val[o] = r.val;
     }
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
-        out.dec[base + k] = s_dec[k];
-        out.rem[base + k] = s_rem[k];
-        out.retry[base + k] = s_retry[k];
-        out.reset[base + k] = s_reset[k];
-        if (out.tok) out.tok[base + k] = s_tok[k];
+        const uint32_t i = base + k;
+        const uint8_t dec = s_dec[k];
+        int64_t rem = 0, retry = 0, reset = 0;
+        double tok = 0.0;
+        if (dec != DEC_INVALID)
+            finish_result(dec, s_val[k], out.ts[i], out.n[i], cfgs[out.cfg[i]], rem, retry, reset, tok);
+        out.dec[i] = dec;
+        out.rem[i] = rem;
+        out.retry[i] = retry;
+        out.reset[i] = reset;
+        if (out.tok) out.tok[i] = tok;
     }
 }
 

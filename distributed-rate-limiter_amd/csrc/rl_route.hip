@@ -6,10 +6,14 @@
 //            scatter into per-owner groups of 32-byte records (ranks from wave
 //            ballots, as rl_sort.h), so each group is one contiguous all-to-all
 //            chunk
-//   merge    the received records in time order (ties: source rank, source
-//            position) by a stable LSD radix sort of (ts - min ts) as 32-bit
-//            keys -- four one-sweep passes of rl_sort.h's k_sort_pass, digit
-//            histograms fused into the key kernel -- then one gather into the
+//   merge    the received records in arrival order at one shared store: by
+//            arrival time (ties: source rank, source position), a record's
+//            arrival time being the running max of ts over its source's
+//            records so far (a server sends its requests in its own order, so
+//            a source's order is always kept); a stable LSD radix sort of
+//            (arrival - earliest) with as many 8-bit passes as the span needs
+//            (rl_sort.h's one-sweep k_sort_pass, up to 48-bit keys; digit
+//            histograms fused into the key kernels), then one gather into the
 //            engine's input arrays
 //   results  / unpack: 32-byte result records gathered by position, written
 //            coalesced
@@ -32,10 +36,11 @@ constexpr int RT_BLOCK = 256;
 constexpr int RT_ITEMS = 4;                    // 1024-request tiles: ~1000 blocks per 1M batch
 constexpr int RT_TILE = RT_BLOCK * RT_ITEMS;   // requests per pack tile
 constexpr int MAX_WORLD = 64;
-constexpr int MERGE_PASSES = 4;                // 32-bit time keys, 8-bit digits
+constexpr int MERGE_PASSES = 6;                // arrival keys of up to 48 bits (spans < 78 h), 8-bit digits
+constexpr int MERGE_KEY_BITS = 8 * MERGE_PASSES;
 
 // router status bits (sticky, cleared by rl_router_sync)
-constexpr uint32_t RS_SPAN = 1u;               // received ts span >= 2^32 ns
+constexpr uint32_t RS_SPAN = 1u;               // received ts span >= 2^48 ns
 
 __device__ inline uint32_t owner_of(uint64_t k, uint32_t world) { return (uint32_t)(mix64(k) >> 32) % world; }
 
@@ -260,45 +265,240 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(uint32_t m, const ui
     }
 }
 
-// ctrl layout of the merge: [0,1] time-key origin (int64), [2] no sort needed, [4] status,
-// [8 .. 8 + 4*256) digit histograms, then 4 tile counters
-constexpr uint32_t MC_MIN = 0, MC_IDENT = 2, MC_STATUS = 4, MC_HIST = 8;
+// ctrl layout of the merge: [0,1] time-key origin lo (int64), [2] no sort (one
+// source), [3] running-max scan needed (a source out of time order), [4]
+// status, [5] sort flags, [6] sort passes, [8 ..) digit histograms of the
+// passes, then one tile counter and one skip flag per pass
+constexpr uint32_t MC_MIN = 0, MC_IDENT = 2, MC_SCAN = 3, MC_STATUS = 4, MC_SFLAGS = 5, MC_NPASS = 6, MC_HIST = 8;
 constexpr uint32_t MC_TILE = MC_HIST + MERGE_PASSES * RADIX;
-constexpr uint32_t MC_WORDS = MC_TILE + MERGE_PASSES;
+constexpr uint32_t MC_SKIP = MC_TILE + MERGE_PASSES;
+constexpr uint32_t MC_WORDS = MC_SKIP + MERGE_PASSES;
+constexpr int MT_ITEMS = 4;                       // consecutive records per thread (merge scans)
+constexpr uint32_t MT_TILE = RT_BLOCK * MT_ITEMS;
+constexpr int SRC_BITS = 58;                      // composite key: source << 58 | (ts - lo)
+constexpr uint64_t OFF_MASK = (1ull << SRC_BITS) - 1;
 
-// 32-bit time key (ts - min) of every received record + the digit histograms
-// of the four passes
-__global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_route_rec* __restrict__ rec,
-                                                         uint32_t* ctrl, uint32_t* __restrict__ kout) {
-    if (ctrl[MC_IDENT]) return;   // no sort: the gather takes the received order
-    __shared__ uint32_t lh[MERGE_PASSES][RADIX];
-    for (int p = 0; p < MERGE_PASSES; p++) lh[p][threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t tmin = *(const int64_t*)(ctrl + MC_MIN);
-    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
-        const uint32_t k = (uint32_t)(uint64_t)(rec[i].ts - tmin);
-        kout[i] = k;
-#pragma unroll
-        for (int p = 0; p < MERGE_PASSES; p++) atomicAdd(&lh[p][(k >> (8 * p)) & (RADIX - 1)], 1u);
+// the merge's plan from the sources' info rows: the time-key origin lo
+// (earliest ts of any source that sent records), whether a sort is needed (more
+// than one source), whether the arrival times need the running-max scan (a
+// source's batch out of time order), and the sort passes the key span needs
+__global__ void k_merge_plan(uint32_t world, const int64_t* __restrict__ info, uint32_t* ctrl) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    uint32_t sources = 0, sorted = 1;
+    for (uint32_t r = 0; r < world; r++) {
+        const int64_t* row = info + (size_t)RL_ROUTE_INFO * r;
+        if (row[0] == 0) continue;
+        sources++;
+        sorted &= row[3] != 0;
+        lo = row[1] < lo ? row[1] : lo;
+        hi = row[2] > hi ? row[2] : hi;
+    }
+    *(int64_t*)(ctrl + MC_MIN) = lo;
+    const uint32_t ident = sources <= 1;
+    ctrl[MC_IDENT] = ident;
+    ctrl[MC_SCAN] = !sorted;
+    const uint64_t span = sources ? (uint64_t)hi - (uint64_t)lo : 0;
+    if (span >> MERGE_KEY_BITS) ctrl[MC_STATUS] |= RS_SPAN;
+    uint32_t np = 0;
+    if (!ident) {
+        np = 1;
+        while (np < (uint32_t)MERGE_PASSES && (span >> (8 * np))) np++;
+    }
+    ctrl[MC_NPASS] = np;
+    for (int p = 0; p < MERGE_PASSES; p++) ctrl[MC_SKIP + p] = (uint32_t)p >= np;
+}
+
+// source rank of received record i (sources are contiguous, in rank order)
+__device__ inline uint64_t src_of(uint32_t i, const uint32_t* s_end, uint32_t world) {
+    uint32_t s = 0;
+    while (s + 1 < world && i >= s_end[s]) s++;
+    return s;
+}
+__device__ inline void load_src_ends(const int64_t* __restrict__ info, uint32_t world, uint32_t* s_end) {
+    if (threadIdx.x == 0) {
+        uint64_t e = 0;
+        for (uint32_t r = 0; r < world; r++) {
+            e += (uint64_t)info[(size_t)RL_ROUTE_INFO * r];
+            s_end[r] = (uint32_t)e;
+        }
     }
     __syncthreads();
-    for (int p = 0; p < MERGE_PASSES; p++) {
-        const uint32_t v = lh[p][threadIdx.x];
-        if (v) atomicAdd(&ctrl[MC_HIST + p * RADIX + threadIdx.x], v);
+}
+// a record's composite arrival key: (source << 58) | (ts - lo).  The running
+// max of the composite along the received buffer restarts at every source
+// (a later source's keys are larger), so it is each source's running max of
+// ts -- the record's arrival time at the store
+__device__ inline uint64_t composite(const rl_route_rec& r, uint64_t src, int64_t lo) {
+    const uint64_t off = (uint64_t)(r.ts - lo);
+    return (src << SRC_BITS) | (off & OFF_MASK);
+}
+
+// per tile of MT_TILE records: the max composite (scan inputs)
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_tmax(uint32_t m, const rl_route_rec* __restrict__ rec,
+                                                         const int64_t* __restrict__ info, uint32_t world,
+                                                         const uint32_t* ctrl, unsigned long long* tmax) {
+    if (!ctrl[MC_SCAN]) return;
+    __shared__ uint32_t s_end[MAX_WORLD];
+    __shared__ unsigned long long s_w[RT_BLOCK / 64];
+    load_src_ends(info, world, s_end);
+    const int64_t lo = *(const int64_t*)(ctrl + MC_MIN);
+    unsigned long long mx = 0;
+#pragma unroll
+    for (int q = 0; q < MT_ITEMS; q++) {
+        const uint32_t i = blockIdx.x * MT_TILE + threadIdx.x * MT_ITEMS + q;
+        if (i < m) {
+            const unsigned long long c = composite(rec[i], src_of(i, s_end, world), lo);
+            mx = c > mx ? c : mx;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(mx, off);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < RT_BLOCK / 64; w++) mx = s_w[w] > mx ? s_w[w] : mx;
+        tmax[blockIdx.x] = mx;
     }
 }
 
-// sorted position p holds received record v[p]: the engine's inputs in
-// order, with the store clock max(floor(ts / 1e6), clock of earlier steps)
+// exclusive running max over the tiles (one block)
+__global__ __launch_bounds__(1024) void k_merge_tscan(uint32_t tiles, const uint32_t* ctrl,
+                                                      unsigned long long* tmax) {
+    if (!ctrl[MC_SCAN]) return;
+    __shared__ unsigned long long s_w[16];
+    __shared__ unsigned long long s_carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t t0 = 0; t0 < tiles; t0 += 1024) {
+        const uint32_t t = t0 + tid;
+        const unsigned long long v = t < tiles ? tmax[t] : 0ull;
+        unsigned long long inc = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc = u > inc ? u : inc;
+        }
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        unsigned long long pre = s_carry;
+        for (uint32_t k = 0; k < w; k++) pre = s_w[k] > pre ? s_w[k] : pre;
+        unsigned long long ex = __shfl_up(inc, 1, 64);
+        ex = lane ? (ex > pre ? ex : pre) : pre;
+        __syncthreads();
+        if (t < tiles) tmax[t] = ex;   // exclusive: the max of every earlier record
+        if (tid == 1023) s_carry = inc > pre ? inc : pre;
+        __syncthreads();
+    }
+}
+
+// arrival key of every received record: kk[i] = (arrival time - lo), the
+// running max of ts over its source's records so far (or ts itself when every
+// source is in time order); the sort's low 32-bit keys and the digit
+// histograms of passes 0-3
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_route_rec* __restrict__ rec,
+                                                         const int64_t* __restrict__ info, uint32_t world,
+                                                         uint32_t* ctrl, const unsigned long long* __restrict__ tpre,
+                                                         unsigned long long* __restrict__ kk,
+                                                         uint32_t* __restrict__ kout) {
+    const bool ident = ctrl[MC_IDENT] != 0, scan = ctrl[MC_SCAN] != 0;
+    if (ident && !scan) return;   // one source in time order: received order, arrival = ts
+    __shared__ uint32_t s_end[MAX_WORLD];
+    __shared__ uint32_t lh[4][RADIX];
+    __shared__ unsigned long long s_w[RT_BLOCK / 64];
+    for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
+    load_src_ends(info, world, s_end);
+    const int64_t lo = *(const int64_t*)(ctrl + MC_MIN);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t i0 = blockIdx.x * MT_TILE + threadIdx.x * MT_ITEMS;
+    unsigned long long c[MT_ITEMS];
+    unsigned long long run = 0;
+#pragma unroll
+    for (int q = 0; q < MT_ITEMS; q++) {
+        const uint32_t i = i0 + q;
+        c[q] = i < m ? composite(rec[i], src_of(i, s_end, world), lo) : 0ull;
+        if (scan) {
+            run = c[q] > run ? c[q] : run;
+            c[q] = run;                                  // inclusive within the thread
+        }
+    }
+    if (scan) {
+        // exclusive max over the earlier threads of the tile and the earlier tiles
+        unsigned long long inc = run;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc = u > inc ? u : inc;
+        }
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        unsigned long long pre = tpre[blockIdx.x];
+        for (uint32_t k = 0; k < w; k++) pre = s_w[k] > pre ? s_w[k] : pre;
+        unsigned long long ex = __shfl_up(inc, 1, 64);
+        ex = lane ? (ex > pre ? ex : pre) : pre;
+#pragma unroll
+        for (int q = 0; q < MT_ITEMS; q++) c[q] = c[q] > ex ? c[q] : ex;
+    }
+    __syncthreads();   // lh zeroed
+#pragma unroll
+    for (int q = 0; q < MT_ITEMS; q++) {
+        const uint32_t i = i0 + q;
+        if (i >= m) continue;
+        const unsigned long long off = c[q] & OFF_MASK;
+        kk[i] = off;
+        if (!ident) {
+            const uint32_t k = (uint32_t)off;
+            kout[i] = k;
+#pragma unroll
+            for (int p = 0; p < 4; p++) atomicAdd(&lh[p][(k >> (8 * p)) & (RADIX - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    if (!ident)
+        for (int p = 0; p < 4; p++) {
+            const uint32_t v = lh[p][threadIdx.x];
+            if (v) atomicAdd(&ctrl[MC_HIST + p * RADIX + threadIdx.x], v);
+        }
+}
+
+// after four passes (data in kin/vin): the high 32 bits of the arrival keys
+// as the next passes' keys, and their digit histograms (spans of 2^32 ns or more)
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_rekey(uint32_t m, uint32_t* ctrl,
+                                                          const unsigned long long* __restrict__ kk,
+                                                          uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin) {
+    if (ctrl[MC_NPASS] <= 4u) return;
+    __shared__ uint32_t lh[MERGE_PASSES - 4][RADIX];
+    for (int p = 0; p < MERGE_PASSES - 4; p++) lh[p][threadIdx.x] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
+        const uint32_t k = (uint32_t)(kk[vin[i]] >> 32);
+        kin[i] = k;
+#pragma unroll
+        for (int p = 0; p < MERGE_PASSES - 4; p++) atomicAdd(&lh[p][(k >> (8 * p)) & (RADIX - 1)], 1u);
+    }
+    __syncthreads();
+    for (int p = 0; p < MERGE_PASSES - 4; p++) {
+        const uint32_t v = lh[p][threadIdx.x];
+        if (v) atomicAdd(&ctrl[MC_HIST + (4 + p) * RADIX + threadIdx.x], v);
+    }
+}
+
+// sorted position p holds received record v[p] (v0 / v1 by the parity of the
+// passes run): the engine's inputs in order, with the store clock
+// max(floor(arrival / 1e6), clock of earlier steps)
 __global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uint32_t* __restrict__ ctrl,
-                                                           const uint32_t* __restrict__ v,
+                                                           const uint32_t* __restrict__ v0,
+                                                           const uint32_t* __restrict__ v1,
                                                            const rl_route_rec* __restrict__ rec,
+                                                           const unsigned long long* __restrict__ kk,
                                                            const int64_t* __restrict__ clock,
                                                            uint64_t* __restrict__ key, int64_t* __restrict__ ts,
                                                            int64_t* __restrict__ n, uint32_t* __restrict__ cfg,
                                                            int64_t* __restrict__ sms, uint32_t* __restrict__ at) {
     const int64_t c0 = *clock;
-    const bool ident = ctrl[MC_IDENT] != 0;
+    const bool ident = ctrl[MC_IDENT] != 0, keyed = !ident || ctrl[MC_SCAN] != 0;
+    const uint32_t* v = (ctrl[MC_NPASS] & 1u) ? v1 : v0;
+    const int64_t lo = *(const int64_t*)(ctrl + MC_MIN);
     for (uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x; p < m; p += gridDim.x * RT_BLOCK) {
         const uint32_t i = ident ? p : v[p];
         const rl_route_rec r = rec[i];
@@ -306,7 +506,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uin
         ts[p] = r.ts;
         n[p] = r.n;
         cfg[p] = r.cfg;
-        const int64_t ms = floor_div(r.ts, 1000000LL);
+        const int64_t arrive = keyed ? (int64_t)((uint64_t)lo + kk[i]) : r.ts;
+        const int64_t ms = floor_div(arrive, 1000000LL);
         sms[p] = ms > c0 ? ms : c0;
         at[i] = p;
     }
@@ -364,6 +565,8 @@ struct rl_router {
     uint32_t* status = nullptr;      // merge: [MERGE_PASSES][tiles][RADIX]
     size_t ctrl_bytes = 0;
     uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr;
+    unsigned long long* kk = nullptr;     // merge: arrival key (arrival - lo) per received record
+    unsigned long long* tmax = nullptr;   // merge: per-tile running-max scan
     uint32_t* d_status = nullptr;    // sticky router status (RS_*)
     int64_t* clock = nullptr;         // the store clock of the next step (ms)
 };
@@ -388,6 +591,8 @@ extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batc
     ok = ok && hipMalloc(&r->psum, sizeof(PackSum) * (ptiles ? ptiles : 1)) == hipSuccess;
     ok = ok && hipMalloc(&r->ctrl, r->ctrl_bytes) == hipSuccess;
     for (uint32_t** p : {&r->k0, &r->k1, &r->v0, &r->v1}) ok = ok && hipMalloc(p, 4 * (size_t)max_recv) == hipSuccess;
+    ok = ok && hipMalloc(&r->kk, 8 * (size_t)max_recv) == hipSuccess;
+    ok = ok && hipMalloc(&r->tmax, 8 * ((size_t)max_recv / MT_TILE + 1)) == hipSuccess;
     ok = ok && hipMalloc(&r->d_status, 4) == hipSuccess && hipMemset(r->d_status, 0, 4) == hipSuccess;
     if (ok && hipMalloc(&r->clock, 8) == hipSuccess) {
         const int64_t lo = INT64_MIN;
@@ -408,6 +613,7 @@ extern "C" int rl_router_destroy(rl_router* r) {
     if (!r) return RL_EINVAL;
     (void)hipSetDevice(r->device);
     for (void* p : {(void*)r->tile_cnt, (void*)r->ctrl, (void*)r->k0, (void*)r->k1, (void*)r->v0, (void*)r->v1,
+                    (void*)r->kk, (void*)r->tmax,
                     (void*)r->d_status, (void*)r->clock, (void*)r->tile_off, (void*)r->psum})
         (void)hipFree(p);
     delete r;
@@ -469,25 +675,6 @@ extern "C" int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const 
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
 }
 
-// the merge's plan from the sources' info rows: the time-key origin (earliest
-// ts of any source that sent records), the span check, and whether the
-// received order already is time order (one source, its batch in order)
-__global__ void k_merge_plan(uint32_t world, const int64_t* __restrict__ info, uint32_t* ctrl) {
-    int64_t lo = INT64_MAX, hi = INT64_MIN;
-    uint32_t sources = 0, sorted = 1;
-    for (uint32_t r = 0; r < world; r++) {
-        const int64_t* row = info + (size_t)RL_ROUTE_INFO * r;
-        if (row[0] == 0) continue;
-        sources++;
-        sorted &= row[3] != 0;
-        lo = row[1] < lo ? row[1] : lo;
-        hi = row[2] > hi ? row[2] : hi;
-    }
-    *(int64_t*)(ctrl + MC_MIN) = lo;
-    ctrl[MC_IDENT] = sources <= 1 && sorted;
-    if (!ctrl[MC_IDENT] && (uint64_t)(hi - lo) > 0xffffffffull) ctrl[MC_STATUS] |= RS_SPAN;
-}
-
 __global__ void k_merge_status(const uint32_t* ctrl, const uint32_t* sort_flags, uint32_t* status) {
     const uint32_t s = (ctrl[MC_STATUS] << 8) | (*sort_flags & EF_LOOKBACK);
     if (s) atomicOr(status, s);
@@ -509,24 +696,31 @@ extern "C" int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* r
     const uint32_t stiles = (m + SORT_TILE - 1) / SORT_TILE;
     if (hipMemsetAsync(r->ctrl, 0, r->ctrl_bytes, s) != hipSuccess) return RL_EDEVICE;
     k_merge_plan<<<1, 1, 0, s>>>(r->world, recv_info, r->ctrl);
-    k_merge_keys<<<grid_for(m), RT_BLOCK, 0, s>>>(m, recv, r->ctrl, r->k0);
-    // look-back timeouts of the sort land in ctrl[MC_STATUS + 1] (EF_LOOKBACK)
-    uint32_t* sflags = r->ctrl + MC_STATUS + 1;
+    const uint32_t mtiles = (m + MT_TILE - 1) / MT_TILE;
+    k_merge_tmax<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, recv_info, r->world, r->ctrl, r->tmax);
+    k_merge_tscan<<<1, 1024, 0, s>>>(mtiles, r->ctrl, r->tmax);
+    k_merge_keys<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, recv_info, r->world, r->ctrl, r->tmax, r->kk, r->k0);
+    // look-back timeouts of the sort land in ctrl[MC_SFLAGS] (EF_LOOKBACK);
+    // passes the key span does not need (and every pass of a one-source
+    // step) are skipped on the device (ctrl[MC_SKIP + p])
+    uint32_t* sflags = r->ctrl + MC_SFLAGS;
     uint32_t *kin = r->k0, *vin = r->v0, *kout = r->k1, *vout = r->v1;
     const size_t max_stiles = (r->max_recv + SORT_TILE - 1) / SORT_TILE;
     for (int p = 0; p < MERGE_PASSES; p++) {
         uint32_t* st = r->status + (size_t)p * max_stiles * RADIX;
+        if (p == 4) k_merge_rekey<<<grid_for(m), RT_BLOCK, 0, s>>>(m, r->ctrl, r->kk, kin, vin);
         if (p == 0)
-            k_sort_pass<true><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p, r->ctrl + MC_HIST + p * RADIX,
-                                                            st, r->ctrl + MC_TILE + p, sflags, r->ctrl + MC_IDENT);
+            k_sort_pass<true><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 0, r->ctrl + MC_HIST, st,
+                                                            r->ctrl + MC_TILE, sflags, r->ctrl + MC_SKIP);
         else
-            k_sort_pass<false><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * p,
-                                                             r->ctrl + MC_HIST + p * RADIX, st,
-                                                             r->ctrl + MC_TILE + p, sflags, r->ctrl + MC_IDENT);
+            k_sort_pass<false><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * (p & 3),
+                                                             r->ctrl + MC_HIST + p * RADIX, st, r->ctrl + MC_TILE + p,
+                                                             sflags, r->ctrl + MC_SKIP + p);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, r->ctrl, vin, recv, r->clock, key, ts, n, cfg, server_ms, at);
+    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, r->ctrl, r->v0, r->v1, recv, r->kk, r->clock, key, ts, n, cfg,
+                                                     server_ms, at);
     k_merge_clock<<<1, 1, 0, s>>>(r->world, recv_info, r->clock);
     k_merge_status<<<1, 1, 0, s>>>(r->ctrl, sflags, r->d_status);
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;

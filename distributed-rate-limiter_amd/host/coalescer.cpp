@@ -111,6 +111,18 @@ public:
         Slot dv;
         carve(d.key, M_, dv);
         const size_t m = s.m;
+        if (m <= zero_copy_max_) {
+            // zero-copy: the kernels read the requests from, and write the
+            // results into, the pinned slot itself (host memory the device
+            // maps).  No hipMemcpyAsync on the submit path: the configs[4]
+            // stalls were the submitter blocked ~8 ms inside those calls
+            // with the device idle (profiles/r3d_stall_trace.json)
+            s.t_h2d = steady_ns();
+            int rc = rl_decide_batch_device(e_, m, s.key, s.ts, s.n, s.cfg, nullptr, s.dec, s.rem, s.retry, s.reset,
+                                            nullptr, os_);
+            if (rc != RL_OK) return rc;
+            return hipEventRecord(d.ev, os_) == hipSuccess ? RL_OK : RL_EDEVICE;
+        }
         bool ok = hipMemcpyAsync(dv.key, s.key, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
         ok &= hipMemcpyAsync(dv.ts, s.ts, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
         ok &= hipMemcpyAsync(dv.n, s.n, 8 * m, hipMemcpyHostToDevice, cs_) == hipSuccess;
@@ -171,6 +183,10 @@ private:
     }
     rl_engine* e_;
     int dev_id_ = 0;             // the engine's device: current when the coalescer is created
+    // batches up to this size run zero-copy on the pinned slot (larger ones:
+    // one H2D copy, device-resident inputs for the grouping's several reads)
+    size_t zero_copy_max_ = getenv("RL_COALESCER_ZC_MAX") ? strtoull(getenv("RL_COALESCER_ZC_MAX"), nullptr, 10)
+                                                          : (size_t)65536;
     hipStream_t cs_ = nullptr, os_ = nullptr;
     std::vector<void*> host_;
     std::vector<Dev> dev_;

@@ -17,8 +17,11 @@
  *            the caller drives the collectives, e.g. torch.distributed "nccl")
  *   owner    rl_route_merge     the received records -- grouped by source rank,
  *                               each group in its source's order -- in the
- *                               order ONE shared store sees them: by request
- *                               time, ties by (source rank, source position);
+ *                               order ONE shared store sees them: by arrival
+ *                               time, ties by (source rank, source position),
+ *                               where a request arrives at the running max of
+ *                               its source's ts so far (each source's own order
+ *                               is kept, also for a batch out of time order);
  *                               written as the key/ts/n/cfg/server_ms arrays
  *                               rl_decide_batch_device takes
  *            rl_decide_batch_device (include/rl_engine.h) on them
@@ -27,16 +30,16 @@
  *   sender   rl_route_unpack    results to the caller's order
  *
  * The store's clock (Redis TTLs) is one clock that never goes back: request
- * p of step b expires keys at server_ms = max(floor(ts_p / 1e6), the latest
- * floor(ts / 1e6) of any request of any rank in steps before b).  Every owner
- * learns each rank's latest ts through the count exchange, so all owners keep
- * the same clock, and per key the clock never decreases (merge order is time
- * order), which is what makes expiry exact (rl_window.h).
+ * p of step b expires keys at server_ms = max(floor(arrival_p / 1e6), the
+ * latest floor(ts / 1e6) of any request of any rank in steps before b).
+ * Every owner learns each rank's latest ts through the count exchange, so all
+ * owners keep the same clock, and per key the clock never decreases (merge
+ * order is arrival order), which is what makes expiry exact (rl_window.h).
  *
  * Every array is device memory; every call is asynchronous on `stream` (a
  * hipStream_t).  Requirement: the timestamps one owner receives in a step
- * span less than 2^32 ns (4.29 s); a violation is reported by rl_router_sync
- * (RL_EINVAL) and the merge order is then unspecified.
+ * span less than 2^48 ns (78 hours); a violation is reported by
+ * rl_router_sync (RL_EINVAL) and the merge order is then unspecified.
  */
 #ifndef RL_ROUTE_H
 #define RL_ROUTE_H
@@ -73,7 +76,7 @@ typedef struct rl_router rl_router;
 int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t max_recv, rl_router** out);
 int rl_router_destroy(rl_router* r);
 /* wait for the router's queued work on `stream`; returns and clears the
- * sticky status (RL_EINVAL: ts span >= 2^32 ns, RL_ETIMEOUT: sort look-back) */
+ * sticky status (RL_EINVAL: ts span >= 2^48 ns, RL_ETIMEOUT: sort look-back) */
 int rl_router_sync(rl_router* r, void* stream);
 
 /* A stream on a hardware queue of its own (CU-masked with every CU, which
@@ -102,9 +105,10 @@ int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts
  * position of received record i in that order.  recv_info: the received
  * send_info rows (source r's at [RL_ROUTE_INFO * r]); they bound the time
  * keys of the merge and advance the store clock after this step.  When only
- * one source sent records and its batch is in time order, the received order
- * already is the decision order and no sort runs.  Call once per step, also
- * when m_recv is 0. */
+ * one source sent records, the received order already is the decision order
+ * and no sort runs (and when every source's batch is in time order, arrival
+ * = ts and no running max is taken).  Call once per step, also when m_recv
+ * is 0. */
 int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info, uint64_t* key,
                    int64_t* ts, int64_t* n, uint32_t* cfg, int64_t* server_ms, uint32_t* at, void* stream);
 

@@ -16,6 +16,16 @@ def _arr(ptr, n, dt):
     return np.ctypeslib.as_array((ct * n).from_address(ptr))
 
 
+def running_max_by_source(ts, src):
+    """per element: the max of ts over the earlier-or-equal elements of the
+    same source (sources contiguous)"""
+    out = np.empty_like(ts)
+    for s in np.unique(src):
+        idx = np.nonzero(src == s)[0]
+        out[idx] = np.maximum.accumulate(ts[idx])
+    return out
+
+
 class NumpyRouteOps:
     def __init__(self, world):
         self.world = world
@@ -48,12 +58,22 @@ class NumpyRouteOps:
         if m == 0:
             return
         rec = _arr(recv, 4 * m, np.int64).reshape(m, 4)
-        o = np.argsort(rec[:, 1], kind="stable")      # time order, ties by received order
+        rows = _arr(info, 4 * self.world, np.int64).reshape(self.world, 4)
+        sent = rows[:, 0] > 0
+        arrive = rec[:, 1].copy()
+        if not np.all(rows[sent, 3] != 0):
+            # a request arrives at the running max of its source's ts so far
+            src = np.minimum(np.searchsorted(np.cumsum(rows[:, 0]), np.arange(m), side="right"), self.world - 1)
+            arrive = running_max_by_source(rec[:, 1], src)
+        if np.count_nonzero(sent) <= 1:
+            o = np.arange(m)                            # one source: its own order
+        else:
+            o = np.argsort(arrive, kind="stable")       # arrival order, ties by received order
         _arr(key, m, np.int64)[:] = rec[o, 0]
         _arr(ts, m, np.int64)[:] = rec[o, 1]
         _arr(n, m, np.int64)[:] = rec[o, 2]
         _arr(cfg, m, np.int32)[:] = (rec[o, 3] & 0xffffffff).astype(np.uint32).view(np.int32)
-        _arr(sms, m, np.int64)[:] = np.maximum(rec[o, 1] // 1_000_000, c0)
+        _arr(sms, m, np.int64)[:] = np.maximum(arrive[o] // 1_000_000, c0)
         a = _arr(at, m, np.int32)
         a[o] = np.arange(m, dtype=np.int32)
 
@@ -93,9 +113,11 @@ def oracle_decide(sim):
 
 def shared_limiter_expectations(all_batches, rank, configs, profile=0):
     """decisions of ONE shared limiter over every rank's batches, step by step,
-    each step in (ts, source rank, source position) order, with the store's
-    clock max(floor(ts / 1e6), the latest of earlier steps) (include/rl_route.h);
-    per step, `rank`'s results in its batch order"""
+    each step in (arrival, source rank, source position) order -- a request's
+    arrival is the running max of ts over the requests its rank sent to the
+    same owner so far -- with the store's clock max(floor(arrival / 1e6), the
+    latest ts of earlier steps) (include/rl_route.h); per step, `rank`'s
+    results in its batch order"""
     import oracle
     ref = oracle.OracleSim(profile)
     for a, L, W in configs:
@@ -108,8 +130,15 @@ def shared_limiter_expectations(all_batches, rank, configs, profile=0):
         U = [np.concatenate([p[f] for p in parts]) for f in range(4)]
         src = np.concatenate([np.full(p[0].size, r) for r, p in enumerate(parts)])
         pos = np.concatenate([np.arange(p[0].size) for p in parts])
-        o = np.lexsort((pos, src, U[1]))
-        sms = np.maximum(U[1][o] // 1_000_000, clock)
+        own = shard.owner_of(U[0].astype(np.uint64), world)
+        arrive = np.empty_like(U[1])
+        for r in range(world):
+            for w in range(world):
+                idx = np.nonzero((src == r) & (own == w))[0]
+                if idx.size:
+                    arrive[idx] = np.maximum.accumulate(U[1][idx])
+        o = np.lexsort((pos, src, arrive))
+        sms = np.maximum(arrive[o] // 1_000_000, clock)
         if U[1].size:
             clock = max(clock, int(U[1].max()) // 1_000_000)
         d, rm, rt, rs, _ = ref.decide(U[0][o], U[1][o], U[2][o], U[3][o], sms)

@@ -128,18 +128,52 @@ def test_merge_single_sorted_source_keeps_order(rl):
     r.close()
 
 
+@pytest.mark.parametrize("span_bits", [33, 41])
+def test_merge_wide_time_spans_and_unsorted_sources(rl, span_bits):
+    """received times spanning more than 2^32 ns (five and six sort passes),
+    three sources out of time order: arrival order against the restatement"""
+    import torch
+
+    import route_ops
+    world = 3
+    m = 30_000
+    rng = np.random.default_rng(span_bits)
+    ts = T0 + rng.integers(0, 1 << span_bits, m).astype(np.int64)
+    rec = np.stack([rng.integers(0, 1 << 62, m), ts, np.ones(m, np.int64), np.arange(m, dtype=np.int64) << 32], 1)
+    cnt = [10_000, 12_000, 8_000]
+    info = np.array([[c, T0, T0 + (1 << span_bits), 0] for c in cnt], np.int64)
+    info[:, 1] = [ts[:10_000].min(), ts[10_000:22_000].min(), ts[22_000:].min()]
+    info[:, 2] = [ts[:10_000].max(), ts[10_000:22_000].max(), ts[22_000:].max()]
+    r = rl.Router(0, world, m, m)
+    ops = route_ops.NumpyRouteOps(world)
+    s = torch.cuda.current_stream().cuda_stream
+    d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
+        [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
+         torch.empty(m, dtype=torch.int32, device="cuda")]
+    h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
+        [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
+    rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
+    r.merge(m, rt.data_ptr(), it.data_ptr(), *[x.data_ptr() for x in d], s)
+    rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
+    ops.merge(m, rh.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
+    assert r.sync(s) == rl.RL_OK
+    for a, b in zip(d, h):
+        assert torch.equal(a.cpu(), b)
+    r.close()
+
+
 def test_merge_reports_a_too_wide_time_span(rl):
     import torch
     m = 5000
-    r = rl.Router(0, 1, m, m)
+    r = rl.Router(0, 2, m, m)
     rec = torch.zeros((m, 4), dtype=torch.int64, device="cuda")
     rec[:, 1] = T0
-    rec[7, 1] = T0 + (1 << 33)
+    rec[7, 1] = T0 + (1 << 49)
     outs = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
             torch.empty(m, dtype=torch.int32, device="cuda")]
     s = torch.cuda.current_stream().cuda_stream
-    info = torch.tensor([[m, T0, T0 + (1 << 33), 0]], dtype=torch.int64, device="cuda")
+    info = torch.tensor([[m - 100, T0, T0 + (1 << 49), 0], [100, T0, T0, 1]], dtype=torch.int64, device="cuda")
     r.merge(m, rec.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs], s)
     assert r.sync(s) == rl.RL_EINVAL
     r.close()
@@ -251,3 +285,24 @@ def test_routed_path_two_ranks_one_gpu():
     """two ranks (two engines, two routers) on the box's one GPU; the
     all-to-alls go through host memory (gloo), the kernels are the GPU's"""
     assert _spawn(2, "gloo", mixed_batches) == {0: True, 1: True}
+
+
+def skewed_batches(rank, nbatch=3, m=60_000, nkeys=20_000):
+    """app servers with skewed clocks (tracegen.skewed_trace): every batch out
+    of time order, spans of minutes (five sort passes), per-key time going
+    back by windows"""
+    import tracegen
+    k, ts, n, cfg, _ = tracegen.skewed_trace(900 + rank, nbatch * m, nkeys, CONFIGS)
+    return [(k[b * m:(b + 1) * m], ts[b * m:(b + 1) * m], n[b * m:(b + 1) * m], cfg[b * m:(b + 1) * m])
+            for b in range(nbatch)]
+
+
+def test_routed_path_one_rank_unsorted_batches():
+    """world size 1 with batches out of time order: the routed path applies a
+    rank's requests in its own order (as rl_decide_batch_device does), with
+    the store clock at each request's arrival (the running max of ts)"""
+    assert _spawn(1, "nccl", skewed_batches) == {0: True}
+
+
+def test_routed_path_two_ranks_unsorted_batches():
+    assert _spawn(2, "gloo", skewed_batches) == {0: True, 1: True}
