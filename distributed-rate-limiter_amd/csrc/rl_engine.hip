@@ -375,8 +375,7 @@ namespace {
 
 constexpr int NSTAGES = 5;
 constexpr uint32_t STAMP_RING = 256;
-constexpr int NSETS = 4;          // batch buffer sets: grouping b+2, b+1 | replay b | finish b-1
-constexpr int NFRONTS = 2;        // grouping streams (consecutive batches alternate)
+constexpr int NSETS = 3;          // batch buffer sets: grouping b+1 | replay b | finish b-1
 constexpr int GROUP_LDS = 4096;   // LDS floor of the grouping / finish kernels (see rl_engine::chain_pad)
 constexpr uint32_t CTRL_HIST = 0;              // [4][256]
 constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
@@ -441,8 +440,7 @@ struct rl_engine {
     // hardware queue each at HIP's default of four queues per process (streams
     // sharing a queue would serialize the replay and the finish)
     hipStream_t stream = nullptr;
-    hipStream_t front[NFRONTS] = {};  // grouping, batch b on front[b mod nfronts]
-    int nfronts = NFRONTS, next_front = 0;
+    hipStream_t front = nullptr;      // grouping
     hipStream_t chain = nullptr;      // replays, in batch order
     hipStream_t tail = nullptr;       // finishes
     hipEvent_t ev_in = nullptr;       // inputs ready (non-pipelined device API, host API)
@@ -613,8 +611,7 @@ static void free_all(rl_engine* e) {
     for (void* p : {(void*)e->s_ts, (void*)e->s_n, (void*)e->s_sms, (void*)e->s_cfg, (void*)e->s_dec, (void*)e->s_tok,
                     (void*)e->s_add, (void*)e->s_th})
         (void)hipFree(p);
-    for (auto f : e->front)
-        if (f) (void)hipStreamDestroy(f);
+    if (e->front) (void)hipStreamDestroy(e->front);
     if (e->chain) (void)hipStreamDestroy(e->chain);
     if (e->tail) (void)hipStreamDestroy(e->tail);
 }
@@ -622,8 +619,7 @@ static void free_all(rl_engine* e) {
 // every queued kernel of the engine has finished (the engine's streams and,
 // through the back_done events, any caller stream a batch was enqueued on)
 static int drain(rl_engine* e) {
-    for (auto f : e->front)
-        if (f) HIPCHK(e, hipStreamSynchronize(f));
+    HIPCHK(e, hipStreamSynchronize(e->front));
     HIPCHK(e, hipStreamSynchronize(e->chain));
     HIPCHK(e, hipStreamSynchronize(e->tail));
     for (auto& B : e->set)
@@ -671,11 +667,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int c = 0; c < ncu; c++)
             if (c % 32 != 31 || ncu < 64) mask[c / 32] |= 1u << (c % 32);
-        if (const char* v = getenv("RL_FRONTS")) e->nfronts = std::max(1, std::min(NFRONTS, atoi(v)));
-        for (int k = 0; k < e->nfronts; k++)
-            if (hipExtStreamCreateWithCUMask(&e->front[k], (uint32_t)mask.size(), mask.data()) != hipSuccess)
-                return bail(RL_EDEVICE);
-        if (hipExtStreamCreateWithCUMask(&e->tail, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+        if (hipExtStreamCreateWithCUMask(&e->front, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
+            hipExtStreamCreateWithCUMask(&e->tail, (uint32_t)mask.size(), mask.data()) != hipSuccess)
             return bail(RL_EDEVICE);
     }
     {
@@ -861,12 +854,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     BatchSet& B = e->set[e->next_set];
     e->last_set = e->next_set;
     e->next_set = (e->next_set + 1) % NSETS;
-    // consecutive batches group on alternating streams: the grouping kernels
-    // are latency-bound (random table probes, look-back sort passes of a few
-    // hundred blocks), so two batches' groupings overlap on the CUs the
-    // replay leaves free
-    hipStream_t f = e->front[e->next_front];
-    e->next_front = (e->next_front + 1) % e->nfronts;
+    hipStream_t f = e->front;
     if (!inputs_ready) {
         HIPCHK(e, hipEventRecord(e->ev_in, s));
         HIPCHK(e, hipStreamWaitEvent(f, e->ev_in, 0));
