@@ -171,43 +171,50 @@ def e2e(args, out_fd):
 
 def grpc_bench(args, out_fd):
     """BASELINE configs[4] end to end: the gRPC server (rl_server.py, a child
-    process that owns the GPU) and open-loop gRPC clients (grpc_load.py,
-    Zipf s=1.5 over 1M keys) at fixed offered rates; latency per decision at
-    the client.  This process never touches the GPU."""
+    process that owns the GPU; native front end by default) and an open-loop
+    gRPC load generator (lib/rl_grpc_load, C++ over HTTP/2; Zipf s=1.5 over 1M
+    keys) at fixed offered rates; latency per RPC at the client from its
+    scheduled send time.  This process never touches the GPU."""
     import subprocess
     py = os.path.join(ROOT, "distributed-rate-limiter_amd", "python")
+    load = os.path.join(ROOT, "distributed-rate-limiter_amd", "lib", "rl_grpc_load")
+    if not os.path.exists(load):
+        raise SystemExit(f"{load} not built (__graft_entry__.build())")
     srv = subprocess.Popen([sys.executable, os.path.join(py, "rl_server.py"), "--address", "127.0.0.1:0",
+                            "--frontend", args.grpc_frontend, "--io-threads", str(args.grpc_io_threads),
                             "--limiter", "default:token_bucket:20:12s", "--tb-capacity", str(1 << 21),
                             "--win-capacity", "1024"], stdout=subprocess.PIPE)
+    levels = []
     try:
         line = srv.stdout.readline().decode()
         if not line.startswith("READY"):
             raise SystemExit(f"server did not start: {line!r}")
         addr = f"127.0.0.1:{int(line.split()[1])}"
-        sys.path.insert(0, py)
-        import contextlib
-        import io
-
-        import grpc_load
-        buf = io.StringIO()
-        with contextlib.redirect_stdout(buf):
-            grpc_load.main(["--addr", addr, "--unary", args.grpc_unary, "--batched", args.grpc_batched,
-                            "--seconds", str(args.seconds), "--procs", str(args.grpc_procs)])
-        r = json.loads(buf.getvalue().strip().splitlines()[-1])
+        shapes = [(float(r), 1) for r in args.grpc_unary.split(",") if r] + \
+                 [(float(r), 256) for r in args.grpc_batched.split(",") if r]
+        for rate, batch in shapes:
+            p = subprocess.run([load, "--addr", addr, "--rate", str(rate), "--seconds", str(args.seconds),
+                                "--batch", str(batch), "--threads", str(args.grpc_threads), "--conns", "4",
+                                "--limiter", "default", "--zipf", "1.5", "--keys", "1000000"],
+                               stdout=subprocess.PIPE, timeout=args.seconds + 120, check=True)
+            levels.append(json.loads(p.stdout.decode().strip().splitlines()[-1]))
+            print(json.dumps(levels[-1]), file=sys.stderr, flush=True)
     finally:
         srv.terminate()
         srv.wait(60)
-    levels = r["levels"]
-    unary = [lv for lv in levels if lv["batch"] == 1 and lv.get("completed_rpcs") and not lv["errors"]
-             and lv["achieved_decisions_per_s"] >= 0.95 * lv["offered_decisions_per_s"]]
-    top = unary[-1] if unary else levels[0]
+    ok = [lv for lv in levels if lv["batch"] == 1 and not lv["errors"] and not lv["unanswered"]
+          and lv["achieved_rpc_per_s"] >= 0.95 * lv["offered_rpc_per_s"]]
+    top = ok[-1] if ok else levels[0]
     out = {"metric": "p99 decision latency at fixed offered load through the gRPC server (configs[4])",
            "value": top.get("p99_us"), "unit": "us", "n_gpus": 1, "higher_is_better": False, "vs_baseline": None,
            "dtype": "f64", "data": "synthetic (Zipf s=1.5 over 1M keys 'user:<id>', fixed-rate open-loop clients)",
            "config": {"workload": "configs[4]: gRPC server (api/proto/ratelimiter.proto), Token Bucket 20/12s, "
-                                  "coalesced GPU batches; unary Allow and AllowBatch RPCs",
+                                  "coalesced GPU batches; unary Allow and AllowBatch (256 AllowN) RPCs",
                       "value_at": {"rpc_per_s": top.get("offered_rpc_per_s"), "batch": top.get("batch")},
-                      "client_processes": args.grpc_procs, "server": "rl_server.py (grpc sync server, 64 workers)"},
+                      "client": f"lib/rl_grpc_load: {args.grpc_threads} threads x 4 HTTP/2 connections",
+                      "server": f"rl_server.py --frontend {args.grpc_frontend} ({args.grpc_io_threads} event loops)"
+                      if args.grpc_frontend == "native" else "rl_server.py --frontend python (grpcio, 64 workers)",
+                      "reference_single_redis_tb_estimate_rps": 35000},
            "levels": levels}
     os.write(out_fd, (json.dumps(out) + "\n").encode())
 
@@ -572,9 +579,11 @@ def main():
     ap.add_argument("--seconds", type=float, default=2.0, help="--e2e / --grpc seconds per level")
     ap.add_argument("--grpc", action="store_true",
                     help="configs[4] through the gRPC server: open-loop gRPC clients at fixed rates")
-    ap.add_argument("--grpc-unary", default="2000,5000,10000", help="--grpc unary Allow RPC rates")
-    ap.add_argument("--grpc-batched", default="500,2000,4000", help="--grpc AllowBatch (256 per RPC) rates")
-    ap.add_argument("--grpc-procs", type=int, default=6, help="--grpc client processes")
+    ap.add_argument("--grpc-unary", default="10000,35000,70000,100000", help="--grpc unary Allow RPC rates")
+    ap.add_argument("--grpc-batched", default="2000,8000", help="--grpc AllowBatch (256 per RPC) rates")
+    ap.add_argument("--grpc-threads", type=int, default=4, help="--grpc load generator threads")
+    ap.add_argument("--grpc-frontend", choices=["native", "python"], default="native", help="--grpc server front end")
+    ap.add_argument("--grpc-io-threads", type=int, default=4, help="--grpc native server event loops")
     args = ap.parse_args()
     if args.e2e:
         return e2e(args, out_fd)

@@ -31,6 +31,7 @@ void Sub::carve(size_t m_) {
     done = waiting = cancelled = dropped = in_queue = waited = false;
     inflight = 0;
     done_ns = submit_ns = 0;
+    tag = nullptr;
     now_ms = 0;
     cap_tb = cap_win = 0;
     info = rl_table_info{};
@@ -289,15 +290,23 @@ void Coalescer::Shutdown() {
             s->done = true;
             s->status = RL_ECLOSED;
             s->cv.notify_all();
+            notify_locked(s);
         }
     }
 }
 
+void Coalescer::SetNotify(NotifyFn fn, void* user) {
+    std::lock_guard<std::mutex> g(mu_);
+    notify_ = fn;
+    notify_user_ = user;
+}
+
 int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
-                      uint64_t* ticket, int64_t deadline) {
+                      uint64_t* ticket, int64_t deadline, void* tag) {
     if (!ticket || (m && (!key || !ts || !n || !cfg)) || deadline < 0) return RL_EINVAL;
     Sub* s = get_sub(m);
     s->deadline = deadline;
+    s->tag = tag;
     if (trace_cap_) s->submit_ns = steady_ns();
     memcpy(s->key, key, 8 * m);
     memcpy(s->ts, ts, 8 * m);
@@ -322,6 +331,7 @@ int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const in
         } else {
             s->done = true;
             s->done_ns = steady_ns();
+            notify_locked(s);
         }
         *ticket = s->first;
         // wake the submitter only when it sleeps: at millions of submissions
@@ -333,9 +343,10 @@ int Coalescer::Submit(size_t m, const uint64_t* key, const int64_t* ts, const in
 }
 
 int Coalescer::SubmitOp(Op op, uint64_t key, int64_t ts, uint32_t cfg, int64_t now_ms, uint64_t cap_tb,
-                        uint64_t cap_win, uint64_t* ticket) {
+                        uint64_t cap_win, uint64_t* ticket, void* tag) {
     Sub* s = get_sub(1);
     s->op = op;
+    s->tag = tag;
     s->key[0] = key;
     s->ts[0] = ts;
     s->n[0] = 1;
@@ -372,6 +383,7 @@ void Coalescer::drop_locked(Sub* s, int code) {
     s->left = 0;
     s->done_ns = steady_ns();
     if (s->waiting) s->cv.notify_all();
+    notify_locked(s);
 }
 
 void Coalescer::maybe_free_locked(Sub* s) {
@@ -610,6 +622,7 @@ void Coalescer::submitter() {
             f->done = true;
             f->done_ns = steady_ns();
             if (f->waiting) f->cv.notify_all();
+            notify_locked(f);
             maybe_free_locked(f);
             // a manual GC invalidates the automatic GC's count
             gc_counted_ = false;
@@ -746,6 +759,7 @@ void Coalescer::completer() {
                     sub->done = true;
                     sub->done_ns = now;
                     if (sub->waiting) sub->cv.notify_all();
+                    notify_locked(sub);
                 }
                 maybe_free_locked(sub);   // orphaned (its waiter gave up) and now complete
             }

@@ -81,6 +81,7 @@ struct Sub {
     uint32_t inflight = 0;        // slot parts launched, not completed
     int64_t done_ns = 0;          // steady clock at completion
     int64_t submit_ns = 0;        // steady clock at Submit (batch trace)
+    void* tag = nullptr;          // the caller's completion tag (SetNotify)
     // OP_INFO / OP_GC arguments and result
     int64_t now_ms = 0;
     uint64_t cap_tb = 0, cap_win = 0;
@@ -113,11 +114,21 @@ public:
     Coalescer(std::unique_ptr<Backend> be, const rl_coalescer_opts& o);
     ~Coalescer();
     int start();
+    // tag: with SetNotify, the completion callback receives it
     int Submit(size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n, const uint32_t* cfg,
-               uint64_t* ticket, int64_t deadline = 0);
+               uint64_t* ticket, int64_t deadline = 0, void* tag = nullptr);
     // a Reset / table count / table GC, queued in sequence order
     int SubmitOp(Op op, uint64_t key, int64_t ts, uint32_t cfg, int64_t now_ms, uint64_t cap_tb,
-                 uint64_t cap_win, uint64_t* ticket);
+                 uint64_t cap_win, uint64_t* ticket, void* tag = nullptr);
+    // Completion callback for submissions made with a tag: fn(user, ticket,
+    // tag) runs once when the submission is done (applied, failed, or dropped
+    // unapplied), on a coalescer thread (or the thread of a Cancel / Wait that
+    // dropped it) WITH THE COALESCER LOCK HELD: it must only hand the ticket
+    // to its owner (an event loop then collects it with Wait(ticket, 0, ...))
+    // and never call back into the coalescer.  Set before the first tagged
+    // submission.
+    using NotifyFn = void (*)(void* user, uint64_t ticket, void* tag);
+    void SetNotify(NotifyFn fn, void* user);
     int Cancel(uint64_t ticket);
     // done_ns (optional): steady-clock completion time of the submission;
     // info (optional): an OP_INFO / OP_GC result
@@ -133,6 +144,12 @@ private:
     void completer();
     // drop a submission none of whose requests was launched: done, unapplied
     void drop_locked(Sub* s, int code);
+    // a submission became done (lock held): the completion callback
+    void notify_locked(Sub* s) {
+        if (notify_ && s->tag) notify_(notify_user_, s->first, s->tag);
+    }
+    NotifyFn notify_ = nullptr;
+    void* notify_user_ = nullptr;
     // free a submission no one references any more (queue, slots, caller)
     void maybe_free_locked(Sub* s);
     // automatic GC before launching `s` (submitter thread, lock not held)

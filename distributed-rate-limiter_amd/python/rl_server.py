@@ -28,7 +28,13 @@ Semantics per RPC follow the Go limiter (internal/ratelimiter):
     GCs them between batches (rl_coalescer_opts.gc_*), so a long-running
     server never fills them.
 
-Run: python rl_server.py --port 8080 --limiter api:token_bucket:20:12s ...
+Two front ends serve the same handlers' semantics: the native one (default,
+include/rl_grpc.h: C++ event loops speaking HTTP/2 + protobuf themselves,
+every RPC submitted to the coalescer as it arrives) and the Python one
+(--frontend python: grpcio's server over RateLimiterService below, which
+also documents the semantics the native server restates).
+
+Run: python rl_server.py --address 127.0.0.1:8080 --limiter api:token_bucket:20:12s ...
 """
 from __future__ import annotations
 
@@ -294,13 +300,38 @@ def serve(service, address, workers=64, grace_s=5.0, ready=None, stop_event=None
     return port
 
 
+def serve_native(co, limiters, address, io_threads=4, isolate=False, grace_s=5.0, ready=None, stop_event=None):
+    """the native front end (include/rl_grpc.h) until SIGTERM / SIGINT (or
+    stop_event): then health NOT_SERVING, stop accepting, answer the RPCs in
+    flight within grace_s"""
+    host, port = address.rsplit(":", 1)
+    srv = rl_amd.GrpcServer(co, [(l.name, l.cfg_id, l.alg, l.limit, l.window_ns, l.prefix, l.fail_open)
+                                 for l in limiters], host=host, port=int(port), io_threads=io_threads,
+                            isolate=isolate)
+    try:
+        if ready:
+            ready(srv.port)
+        stop = stop_event or threading.Event()
+        if threading.current_thread() is threading.main_thread():
+            for sig in (signal.SIGTERM, signal.SIGINT):
+                signal.signal(sig, lambda *_: stop.set())
+        stop.wait()
+        srv.shutdown(grace_s)
+    finally:
+        srv.close()
+    return srv.port
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="rate limiter gRPC server (MI355X engine)")
     ap.add_argument("--address", default="127.0.0.1:8080", help="listen address (docs/ARCHITECTURE.md: port 8080)")
     ap.add_argument("--limiter", action="append", default=[],
                     help="name:algorithm:limit:window[:prefix[:fail_open]], repeatable")
     ap.add_argument("--device", type=int, default=0)
-    ap.add_argument("--workers", type=int, default=64)
+    ap.add_argument("--frontend", choices=["native", "python"], default="native",
+                    help="native: C++ HTTP/2 event loops (include/rl_grpc.h); python: grpcio server")
+    ap.add_argument("--io-threads", type=int, default=4, help="native front end: event-loop threads")
+    ap.add_argument("--workers", type=int, default=64, help="python front end: handler threads")
     ap.add_argument("--max-batch", type=int, default=1 << 16)
     ap.add_argument("--tb-capacity", type=int, default=1 << 22)
     ap.add_argument("--win-capacity", type=int, default=1 << 22)
@@ -315,11 +346,20 @@ def main(argv=None):
     specs = args.limiter or ["default:token_bucket:20:12s"]
     limiters = [Limiter.parse(s) for s in specs]
     be = GpuBackend(args.device, args.tb_capacity, args.win_capacity, args.max_batch)
-    svc = RateLimiterService(limiters, None, be.register, isolate=args.isolate_limiters)
-    svc.co = be.start(args.max_batch, int(args.gc_interval_ms * 1e6), args.gc_margin_ms)
-    print(f"rate limiter gRPC server on {args.address}: " + ", ".join(specs), file=sys.stderr, flush=True)
+    print(f"rate limiter gRPC server on {args.address} ({args.frontend} front end): " + ", ".join(specs),
+          file=sys.stderr, flush=True)
     try:
-        serve(svc, args.address, args.workers, ready=lambda p: print(f"READY {p}", flush=True))
+        if args.frontend == "native":
+            for lim in limiters:
+                lim.cfg_id = be.register(lim.alg, lim.limit, lim.window_ns)
+            co = be.start(args.max_batch, int(args.gc_interval_ms * 1e6),
+                          args.gc_margin_ms)
+            serve_native(co, limiters, args.address, args.io_threads, args.isolate_limiters,
+                         ready=lambda p: print(f"READY {p}", flush=True))
+        else:
+            svc = RateLimiterService(limiters, None, be.register, isolate=args.isolate_limiters)
+            svc.co = be.start(args.max_batch, int(args.gc_interval_ms * 1e6), args.gc_margin_ms)
+            serve(svc, args.address, args.workers, ready=lambda p: print(f"READY {p}", flush=True))
     finally:
         be.close()
     return 0

@@ -11,13 +11,20 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include"))) if h.endswith(".h")]
 
 
-def declared_functions():
+def declared_functions(header_filter=None):
     names = []
     for h in HEADERS:
+        if header_filter and not header_filter(os.path.basename(h)):
+            continue
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names += re.findall(r"^\s*(?:int|rl_engine\s*\*)\s+(rll?_\w+)\s*\(", src, flags=re.M)
     return sorted(set(names))
+
+
+# include/rl_grpc.h is lib/librl_grpc.so (the native gRPC front end); every
+# other header is lib/librl_amd.so
+GRPC_H = "rl_grpc.h"
 
 
 def test_headers_declare_the_boundary():
@@ -29,9 +36,14 @@ def test_headers_declare_the_boundary():
         assert must in names
 
 
-@pytest.mark.parametrize("name", declared_functions())
+@pytest.mark.parametrize("name", declared_functions(lambda h: h != GRPC_H))
 def test_symbol_exported(rl, name):
     assert hasattr(rl.lib, name), name
+
+
+@pytest.mark.parametrize("name", declared_functions(lambda h: h == GRPC_H))
+def test_grpc_symbol_exported(rl, name):
+    assert hasattr(rl.grpc_lib(), name), name
 
 
 def test_q14_host_instantiation(rl):
