@@ -265,48 +265,26 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scatter(uint32_t m, const ui
     }
 }
 
-// ctrl layout of the merge: [0,1] time-key origin lo (int64), [2] no sort (one
-// source), [3] running-max scan needed (a source out of time order), [4]
-// status, [5] sort flags, [6] sort passes, [8 ..) digit histograms of the
-// passes, then one tile counter and one skip flag per pass
-constexpr uint32_t MC_MIN = 0, MC_IDENT = 2, MC_SCAN = 3, MC_STATUS = 4, MC_SFLAGS = 5, MC_NPASS = 6, MC_HIST = 8;
+// The merge's plan, made on the host from the received info rows (the caller
+// read them to size the record exchange): which kernels run at all
+struct MergePlan {
+    int64_t lo;         // time-key origin: earliest ts of any source that sent records
+    int64_t clock;      // the store clock of the earlier steps (ms)
+    uint32_t ident;     // at most one source sent records: received order is the decision order
+    uint32_t scan;      // a source's batch is out of time order: arrival = running max of its ts
+    uint32_t npass;     // 8-bit sort passes the arrival-key span needs (0 when ident)
+};
+
+// ctrl layout: digit histograms of the passes, one tile counter per pass, the
+// sort's look-back flags; the passes' look-back status follows, npass x tiles
+constexpr uint32_t MC_HIST = 0;
 constexpr uint32_t MC_TILE = MC_HIST + MERGE_PASSES * RADIX;
-constexpr uint32_t MC_SKIP = MC_TILE + MERGE_PASSES;
-constexpr uint32_t MC_WORDS = MC_SKIP + MERGE_PASSES;
+constexpr uint32_t MC_SFLAGS = MC_TILE + MERGE_PASSES;
+constexpr uint32_t MC_WORDS = (MC_SFLAGS + 1 + 63) & ~63u;
 constexpr int MT_ITEMS = 4;                       // consecutive records per thread (merge scans)
 constexpr uint32_t MT_TILE = RT_BLOCK * MT_ITEMS;
 constexpr int SRC_BITS = 58;                      // composite key: source << 58 | (ts - lo)
 constexpr uint64_t OFF_MASK = (1ull << SRC_BITS) - 1;
-
-// the merge's plan from the sources' info rows: the time-key origin lo
-// (earliest ts of any source that sent records), whether a sort is needed (more
-// than one source), whether the arrival times need the running-max scan (a
-// source's batch out of time order), and the sort passes the key span needs
-__global__ void k_merge_plan(uint32_t world, const int64_t* __restrict__ info, uint32_t* ctrl) {
-    int64_t lo = INT64_MAX, hi = INT64_MIN;
-    uint32_t sources = 0, sorted = 1;
-    for (uint32_t r = 0; r < world; r++) {
-        const int64_t* row = info + (size_t)RL_ROUTE_INFO * r;
-        if (row[0] == 0) continue;
-        sources++;
-        sorted &= row[3] != 0;
-        lo = row[1] < lo ? row[1] : lo;
-        hi = row[2] > hi ? row[2] : hi;
-    }
-    *(int64_t*)(ctrl + MC_MIN) = lo;
-    const uint32_t ident = sources <= 1;
-    ctrl[MC_IDENT] = ident;
-    ctrl[MC_SCAN] = !sorted;
-    const uint64_t span = sources ? (uint64_t)hi - (uint64_t)lo : 0;
-    if (span >> MERGE_KEY_BITS) ctrl[MC_STATUS] |= RS_SPAN;
-    uint32_t np = 0;
-    if (!ident) {
-        np = 1;
-        while (np < (uint32_t)MERGE_PASSES && (span >> (8 * np))) np++;
-    }
-    ctrl[MC_NPASS] = np;
-    for (int p = 0; p < MERGE_PASSES; p++) ctrl[MC_SKIP + p] = (uint32_t)p >= np;
-}
 
 // source rank of received record i (sources are contiguous, in rank order)
 __device__ inline uint64_t src_of(uint32_t i, const uint32_t* s_end, uint32_t world) {
@@ -333,21 +311,19 @@ __device__ inline uint64_t composite(const rl_route_rec& r, uint64_t src, int64_
     return (src << SRC_BITS) | (off & OFF_MASK);
 }
 
-// per tile of MT_TILE records: the max composite (scan inputs)
+// per tile of MT_TILE records: the max composite (scan inputs; plan.scan only)
 __global__ __launch_bounds__(RT_BLOCK) void k_merge_tmax(uint32_t m, const rl_route_rec* __restrict__ rec,
                                                          const int64_t* __restrict__ info, uint32_t world,
-                                                         const uint32_t* ctrl, unsigned long long* tmax) {
-    if (!ctrl[MC_SCAN]) return;
+                                                         MergePlan plan, unsigned long long* tmax) {
     __shared__ uint32_t s_end[MAX_WORLD];
     __shared__ unsigned long long s_w[RT_BLOCK / 64];
     load_src_ends(info, world, s_end);
-    const int64_t lo = *(const int64_t*)(ctrl + MC_MIN);
     unsigned long long mx = 0;
 #pragma unroll
     for (int q = 0; q < MT_ITEMS; q++) {
         const uint32_t i = blockIdx.x * MT_TILE + threadIdx.x * MT_ITEMS + q;
         if (i < m) {
-            const unsigned long long c = composite(rec[i], src_of(i, s_end, world), lo);
+            const unsigned long long c = composite(rec[i], src_of(i, s_end, world), plan.lo);
             mx = c > mx ? c : mx;
         }
     }
@@ -363,10 +339,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_tmax(uint32_t m, const rl_ro
     }
 }
 
-// exclusive running max over the tiles (one block)
-__global__ __launch_bounds__(1024) void k_merge_tscan(uint32_t tiles, const uint32_t* ctrl,
-                                                      unsigned long long* tmax) {
-    if (!ctrl[MC_SCAN]) return;
+// exclusive running max over the tiles (one block; plan.scan only)
+__global__ __launch_bounds__(1024) void k_merge_tscan(uint32_t tiles, unsigned long long* tmax) {
     __shared__ unsigned long long s_w[16];
     __shared__ unsigned long long s_carry;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -395,21 +369,20 @@ __global__ __launch_bounds__(1024) void k_merge_tscan(uint32_t tiles, const uint
 
 // arrival key of every received record: kk[i] = (arrival time - lo), the
 // running max of ts over its source's records so far (or ts itself when every
-// source is in time order); the sort's low 32-bit keys and the digit
-// histograms of passes 0-3
+// source is in time order); with a sort (not ident), the sort's low 32-bit
+// keys and the digit histograms of passes 0-3
 __global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_route_rec* __restrict__ rec,
                                                          const int64_t* __restrict__ info, uint32_t world,
-                                                         uint32_t* ctrl, const unsigned long long* __restrict__ tpre,
+                                                         MergePlan plan, uint32_t* ctrl,
+                                                         const unsigned long long* __restrict__ tpre,
                                                          unsigned long long* __restrict__ kk,
                                                          uint32_t* __restrict__ kout) {
-    const bool ident = ctrl[MC_IDENT] != 0, scan = ctrl[MC_SCAN] != 0;
-    if (ident && !scan) return;   // one source in time order: received order, arrival = ts
+    const bool ident = plan.ident != 0, scan = plan.scan != 0;
     __shared__ uint32_t s_end[MAX_WORLD];
     __shared__ uint32_t lh[4][RADIX];
     __shared__ unsigned long long s_w[RT_BLOCK / 64];
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
     load_src_ends(info, world, s_end);
-    const int64_t lo = *(const int64_t*)(ctrl + MC_MIN);
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t i0 = blockIdx.x * MT_TILE + threadIdx.x * MT_ITEMS;
     unsigned long long c[MT_ITEMS];
@@ -417,7 +390,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_ro
 #pragma unroll
     for (int q = 0; q < MT_ITEMS; q++) {
         const uint32_t i = i0 + q;
-        c[q] = i < m ? composite(rec[i], src_of(i, s_end, world), lo) : 0ull;
+        c[q] = i < m ? composite(rec[i], src_of(i, s_end, world), plan.lo) : 0ull;
         if (scan) {
             run = c[q] > run ? c[q] : run;
             c[q] = run;                                  // inclusive within the thread
@@ -466,7 +439,6 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_keys(uint32_t m, const rl_ro
 __global__ __launch_bounds__(RT_BLOCK) void k_merge_rekey(uint32_t m, uint32_t* ctrl,
                                                           const unsigned long long* __restrict__ kk,
                                                           uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin) {
-    if (ctrl[MC_NPASS] <= 4u) return;
     __shared__ uint32_t lh[MERGE_PASSES - 4][RADIX];
     for (int p = 0; p < MERGE_PASSES - 4; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
@@ -483,22 +455,17 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_rekey(uint32_t m, uint32_t* 
     }
 }
 
-// sorted position p holds received record v[p] (v0 / v1 by the parity of the
-// passes run): the engine's inputs in order, with the store clock
-// max(floor(arrival / 1e6), clock of earlier steps)
-__global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uint32_t* __restrict__ ctrl,
-                                                           const uint32_t* __restrict__ v0,
-                                                           const uint32_t* __restrict__ v1,
+// sorted position p holds received record v[p] (identity when ident): the
+// engine's inputs in order, with the store clock max(floor(arrival / 1e6),
+// clock of earlier steps)
+__global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, MergePlan plan, const uint32_t* __restrict__ v,
                                                            const rl_route_rec* __restrict__ rec,
                                                            const unsigned long long* __restrict__ kk,
-                                                           const int64_t* __restrict__ clock,
                                                            uint64_t* __restrict__ key, int64_t* __restrict__ ts,
                                                            int64_t* __restrict__ n, uint32_t* __restrict__ cfg,
                                                            int64_t* __restrict__ sms, uint32_t* __restrict__ at) {
-    const int64_t c0 = *clock;
-    const bool ident = ctrl[MC_IDENT] != 0, keyed = !ident || ctrl[MC_SCAN] != 0;
-    const uint32_t* v = (ctrl[MC_NPASS] & 1u) ? v1 : v0;
-    const int64_t lo = *(const int64_t*)(ctrl + MC_MIN);
+    const bool ident = plan.ident != 0, keyed = !ident || plan.scan != 0;
+    const int64_t c0 = plan.clock;
     for (uint32_t p = blockIdx.x * RT_BLOCK + threadIdx.x; p < m; p += gridDim.x * RT_BLOCK) {
         const uint32_t i = ident ? p : v[p];
         const rl_route_rec r = rec[i];
@@ -506,23 +473,11 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, const uin
         ts[p] = r.ts;
         n[p] = r.n;
         cfg[p] = r.cfg;
-        const int64_t arrive = keyed ? (int64_t)((uint64_t)lo + kk[i]) : r.ts;
+        const int64_t arrive = keyed ? (int64_t)((uint64_t)plan.lo + kk[i]) : r.ts;
         const int64_t ms = floor_div(arrive, 1000000LL);
         sms[p] = ms > c0 ? ms : c0;
         at[i] = p;
     }
-}
-
-// after a step: clock = max(clock, floor(latest ts of any rank / 1e6))
-__global__ void k_merge_clock(uint32_t world, const int64_t* __restrict__ info, int64_t* clock) {
-    int64_t c = *clock;
-    for (uint32_t r = 0; r < world; r++) {
-        const int64_t latest = info[(size_t)RL_ROUTE_INFO * r + 2];
-        if (latest == INT64_MIN) continue;   // that rank's batch was empty
-        const int64_t ms = floor_div(latest, 1000000LL);
-        c = ms > c ? ms : c;
-    }
-    *clock = c;
 }
 
 __global__ __launch_bounds__(RT_BLOCK) void k_route_results(uint32_t m, const uint32_t* __restrict__ at,
@@ -562,13 +517,13 @@ struct rl_router {
     uint32_t* tile_off = nullptr;    // pack: [tiles][world] output offsets
     PackSum* psum = nullptr;         // pack: per-tile summaries [tiles]
     uint32_t* ctrl = nullptr;        // merge: MC_* words + look-back status
-    uint32_t* status = nullptr;      // merge: [MERGE_PASSES][tiles][RADIX]
-    size_t ctrl_bytes = 0;
+    uint32_t* status = nullptr;      // merge: [npass][tiles][RADIX] of the current step
     uint32_t *k0 = nullptr, *k1 = nullptr, *v0 = nullptr, *v1 = nullptr;
     unsigned long long* kk = nullptr;     // merge: arrival key (arrival - lo) per received record
     unsigned long long* tmax = nullptr;   // merge: per-tile running-max scan
-    uint32_t* d_status = nullptr;    // sticky router status (RS_*)
-    int64_t* clock = nullptr;         // the store clock of the next step (ms)
+    uint32_t* d_status = nullptr;    // sticky router status: the sort's look-back flags
+    uint32_t host_status = 0;        // sticky router status found by the host plan (RS_*)
+    int64_t clock = INT64_MIN;        // the store clock of the next step (ms), kept in enqueue order
 };
 
 extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t max_recv,
@@ -585,21 +540,14 @@ extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batc
     r->max_recv = max_recv;
     const size_t ptiles = (max_batch + RT_TILE - 1) / RT_TILE;
     const size_t stiles = (max_recv + SORT_TILE - 1) / SORT_TILE;
-    r->ctrl_bytes = 4 * (MC_WORDS + (size_t)MERGE_PASSES * stiles * RADIX);
     bool ok = hipMalloc(&r->tile_cnt, 4 * ptiles * world) == hipSuccess;
     ok = ok && hipMalloc(&r->tile_off, 4 * ptiles * world) == hipSuccess;
     ok = ok && hipMalloc(&r->psum, sizeof(PackSum) * (ptiles ? ptiles : 1)) == hipSuccess;
-    ok = ok && hipMalloc(&r->ctrl, r->ctrl_bytes) == hipSuccess;
+    ok = ok && hipMalloc(&r->ctrl, 4 * (MC_WORDS + (size_t)MERGE_PASSES * stiles * RADIX)) == hipSuccess;
     for (uint32_t** p : {&r->k0, &r->k1, &r->v0, &r->v1}) ok = ok && hipMalloc(p, 4 * (size_t)max_recv) == hipSuccess;
     ok = ok && hipMalloc(&r->kk, 8 * (size_t)max_recv) == hipSuccess;
     ok = ok && hipMalloc(&r->tmax, 8 * ((size_t)max_recv / MT_TILE + 1)) == hipSuccess;
     ok = ok && hipMalloc(&r->d_status, 4) == hipSuccess && hipMemset(r->d_status, 0, 4) == hipSuccess;
-    if (ok && hipMalloc(&r->clock, 8) == hipSuccess) {
-        const int64_t lo = INT64_MIN;
-        ok = hipMemcpy(r->clock, &lo, 8, hipMemcpyHostToDevice) == hipSuccess;
-    } else {
-        ok = false;
-    }
     if (!ok) {
         rl_router_destroy(r);
         return RL_ENOMEM;
@@ -614,7 +562,7 @@ extern "C" int rl_router_destroy(rl_router* r) {
     (void)hipSetDevice(r->device);
     for (void* p : {(void*)r->tile_cnt, (void*)r->ctrl, (void*)r->k0, (void*)r->k1, (void*)r->v0, (void*)r->v1,
                     (void*)r->kk, (void*)r->tmax,
-                    (void*)r->d_status, (void*)r->clock, (void*)r->tile_off, (void*)r->psum})
+                    (void*)r->d_status, (void*)r->tile_off, (void*)r->psum})
         (void)hipFree(p);
     delete r;
     return RL_OK;
@@ -627,8 +575,10 @@ extern "C" int rl_router_sync(rl_router* r, void* stream) {
     uint32_t s = 0;
     if (hipMemcpy(&s, r->d_status, 4, hipMemcpyDeviceToHost) != hipSuccess) return RL_EDEVICE;
     if (hipMemset(r->d_status, 0, 4) != hipSuccess) return RL_EDEVICE;
+    const uint32_t h = r->host_status;
+    r->host_status = 0;
     if (s & EF_LOOKBACK) return RL_ETIMEOUT;
-    if (s & (RS_SPAN << 8)) return RL_EINVAL;
+    if (h & RS_SPAN) return RL_EINVAL;
     return RL_OK;
 }
 
@@ -675,54 +625,74 @@ extern "C" int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const 
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
 }
 
-__global__ void k_merge_status(const uint32_t* ctrl, const uint32_t* sort_flags, uint32_t* status) {
-    const uint32_t s = (ctrl[MC_STATUS] << 8) | (*sort_flags & EF_LOOKBACK);
-    if (s) atomicOr(status, s);
+__global__ void k_merge_status(const uint32_t* sort_flags, uint32_t* status) {
+    const uint32_t f = *sort_flags & EF_LOOKBACK;
+    if (f) atomicOr(status, f);
 }
 
 extern "C" int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info,
-                              uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg, int64_t* server_ms, uint32_t* at,
-                              void* stream) {
-    if (!r || !recv_info || m_recv > r->max_recv ||
+                              const int64_t* recv_info_host, uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg,
+                              int64_t* server_ms, uint32_t* at, void* stream) {
+    if (!r || !recv_info || !recv_info_host || m_recv > r->max_recv ||
         (m_recv && (!recv || !key || !ts || !n || !cfg || !server_ms || !at)))
         return RL_EINVAL;
     (void)hipSetDevice(r->device);
     hipStream_t s = (hipStream_t)stream;
-    if (!m_recv) {
-        k_merge_clock<<<1, 1, 0, s>>>(r->world, recv_info, r->clock);
-        return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+    // the plan, on the host: the time-key origin and span of the sources that
+    // sent records, whether a source is out of time order, the passes
+    int64_t lo = INT64_MAX, hi = INT64_MIN, clock_next = r->clock;
+    uint32_t sources = 0, sorted = 1;
+    for (uint32_t q = 0; q < r->world; q++) {
+        const int64_t* row = recv_info_host + (size_t)RL_ROUTE_INFO * q;
+        if (row[2] != INT64_MIN) {   // after this step: clock = max(clock, floor(latest ts / 1e6))
+            const int64_t ms = floor_div(row[2], 1000000LL);
+            clock_next = ms > clock_next ? ms : clock_next;
+        }
+        if (row[0] == 0) continue;
+        sources++;
+        sorted &= row[3] != 0;
+        lo = row[1] < lo ? row[1] : lo;
+        hi = row[2] > hi ? row[2] : hi;
     }
+    MergePlan plan{lo, r->clock, sources <= 1 ? 1u : 0u, sorted ? 0u : 1u, 0u};
+    r->clock = clock_next;
     const uint32_t m = (uint32_t)m_recv;
-    const uint32_t stiles = (m + SORT_TILE - 1) / SORT_TILE;
-    if (hipMemsetAsync(r->ctrl, 0, r->ctrl_bytes, s) != hipSuccess) return RL_EDEVICE;
-    k_merge_plan<<<1, 1, 0, s>>>(r->world, recv_info, r->ctrl);
+    if (!m) return RL_OK;
+    const uint64_t span = (uint64_t)hi - (uint64_t)lo;
+    if (span >> MERGE_KEY_BITS) r->host_status |= RS_SPAN;
+    if (!plan.ident) {
+        plan.npass = 1;
+        while (plan.npass < (uint32_t)MERGE_PASSES && (span >> (8 * plan.npass))) plan.npass++;
+    }
     const uint32_t mtiles = (m + MT_TILE - 1) / MT_TILE;
-    k_merge_tmax<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, recv_info, r->world, r->ctrl, r->tmax);
-    k_merge_tscan<<<1, 1024, 0, s>>>(mtiles, r->ctrl, r->tmax);
-    k_merge_keys<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, recv_info, r->world, r->ctrl, r->tmax, r->kk, r->k0);
-    // look-back timeouts of the sort land in ctrl[MC_SFLAGS] (EF_LOOKBACK);
-    // passes the key span does not need (and every pass of a one-source
-    // step) are skipped on the device (ctrl[MC_SKIP + p])
+    const uint32_t stiles = (m + SORT_TILE - 1) / SORT_TILE;
+    if (!plan.ident || plan.scan) {
+        // the control words and the look-back status of the passes this step runs
+        const size_t words = MC_WORDS + (size_t)plan.npass * stiles * RADIX;
+        if (hipMemsetAsync(r->ctrl, 0, 4 * words, s) != hipSuccess) return RL_EDEVICE;
+        if (plan.scan) {
+            k_merge_tmax<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, recv_info, r->world, plan, r->tmax);
+            k_merge_tscan<<<1, 1024, 0, s>>>(mtiles, r->tmax);
+        }
+        k_merge_keys<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, recv_info, r->world, plan, r->ctrl, r->tmax, r->kk, r->k0);
+    }
     uint32_t* sflags = r->ctrl + MC_SFLAGS;
     uint32_t *kin = r->k0, *vin = r->v0, *kout = r->k1, *vout = r->v1;
-    const size_t max_stiles = (r->max_recv + SORT_TILE - 1) / SORT_TILE;
-    for (int p = 0; p < MERGE_PASSES; p++) {
-        uint32_t* st = r->status + (size_t)p * max_stiles * RADIX;
+    for (uint32_t p = 0; p < plan.npass; p++) {
+        uint32_t* st = r->status + (size_t)p * stiles * RADIX;
         if (p == 4) k_merge_rekey<<<grid_for(m), RT_BLOCK, 0, s>>>(m, r->ctrl, r->kk, kin, vin);
         if (p == 0)
             k_sort_pass<true><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 0, r->ctrl + MC_HIST, st,
-                                                            r->ctrl + MC_TILE, sflags, r->ctrl + MC_SKIP);
+                                                            r->ctrl + MC_TILE, sflags);
         else
             k_sort_pass<false><<<stiles, SORT_BLOCK, 0, s>>>(kin, vin, kout, vout, m, 8 * (p & 3),
                                                              r->ctrl + MC_HIST + p * RADIX, st, r->ctrl + MC_TILE + p,
-                                                             sflags, r->ctrl + MC_SKIP + p);
+                                                             sflags);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, r->ctrl, r->v0, r->v1, recv, r->kk, r->clock, key, ts, n, cfg,
-                                                     server_ms, at);
-    k_merge_clock<<<1, 1, 0, s>>>(r->world, recv_info, r->clock);
-    k_merge_status<<<1, 1, 0, s>>>(r->ctrl, sflags, r->d_status);
+    k_merge_gather<<<grid_for(m), RT_BLOCK, 0, s>>>(m, plan, vin, recv, r->kk, key, ts, n, cfg, server_ms, at);
+    if (plan.npass) k_merge_status<<<1, 1, 0, s>>>(sflags, r->d_status);
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
 }
 

@@ -196,7 +196,7 @@ _sig = {
     "rl_stream_create_dedicated": (C.c_int, [C.c_int32, C.POINTER(vp)]),
     "rl_stream_destroy": (C.c_int, [vp]),
     "rl_route_pack": (C.c_int, [vp, C.c_size_t] + [vp] * 8),
-    "rl_route_merge": (C.c_int, [vp, C.c_size_t] + [vp] * 9),
+    "rl_route_merge": (C.c_int, [vp, C.c_size_t] + [vp] * 10),
     "rl_route_results": (C.c_int, [C.c_size_t] + [vp] * 7),
     "rl_route_unpack": (C.c_int, [C.c_size_t] + [vp] * 7),
 }
@@ -408,8 +408,9 @@ class Router:
     def pack(self, m, key, ts, n, cfg, send, send_info, slot, stream):
         self._chk(lib.rl_route_pack(self.h, m, key, ts, n, cfg, send, send_info, slot, stream), "rl_route_pack")
 
-    def merge(self, m_recv, recv, recv_info, key, ts, n, cfg, sms, at, stream):
-        self._chk(lib.rl_route_merge(self.h, m_recv, recv, recv_info, key, ts, n, cfg, sms, at, stream),
+    def merge(self, m_recv, recv, recv_info, recv_info_host, key, ts, n, cfg, sms, at, stream):
+        self._chk(lib.rl_route_merge(self.h, m_recv, recv, recv_info, recv_info_host, key, ts, n, cfg, sms, at,
+                                     stream),
                   "rl_route_merge")
 
     @staticmethod

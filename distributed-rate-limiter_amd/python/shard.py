@@ -216,8 +216,9 @@ class RoutedPipeline:
         self.last_recv = tot
         p = self._p
         def merge(stream):
-            self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]),
-                           p(s["sms"]), p(s["at"]), self._sp(stream))
+            # the received info rows on the host too (read above): the merge is planned there
+            self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["cnt_h"][1]), p(s["key"]), p(s["ts"]), p(s["n"]),
+                           p(s["cfg"]), p(s["sms"]), p(s["at"]), self._sp(stream))
 
         with _ctx(self.R):
             if self.C is not self.R:

@@ -103,14 +103,18 @@ int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts
 /* owner: recv[m_recv] (grouped by source rank) -> the decision order; writes
  * key/ts/n/cfg/server_ms[m_recv] for rl_decide_batch_device and at[i] = the
  * position of received record i in that order.  recv_info: the received
- * send_info rows (source r's at [RL_ROUTE_INFO * r]); they bound the time
- * keys of the merge and advance the store clock after this step.  When only
+ * send_info rows (source r's at [RL_ROUTE_INFO * r]) in device memory, and
+ * recv_info_host: the same rows on the host (the caller read them to size the
+ * record exchange).  The merge is planned on the host from them: when only
  * one source sent records, the received order already is the decision order
- * and no sort runs (and when every source's batch is in time order, arrival
- * = ts and no running max is taken).  Call once per step, also when m_recv
- * is 0. */
-int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info, uint64_t* key,
-                   int64_t* ts, int64_t* n, uint32_t* cfg, int64_t* server_ms, uint32_t* at, void* stream);
+ * and the merge is one gather kernel (when every source's batch is in time
+ * order, arrival = ts and no running max is taken); otherwise only the sort
+ * passes the step's time span needs are launched.  The rows also advance the
+ * store clock after this step.  Call once per step, in step order, also when
+ * m_recv is 0. */
+int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info,
+                   const int64_t* recv_info_host, uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg,
+                   int64_t* server_ms, uint32_t* at, void* stream);
 
 /* owner: decisions (in the merge order) -> res[i] for received record i */
 int rl_route_results(size_t m_recv, const uint32_t* at, const uint8_t* decision, const int64_t* remaining,

@@ -49,7 +49,7 @@ class NumpyRouteOps:
         sl = _arr(slot, m, np.int32)
         sl[order] = np.arange(m, dtype=np.int32)
 
-    def merge(self, m, recv, info, key, ts, n, cfg, sms, at, stream):
+    def merge(self, m, recv, info, info_host, key, ts, n, cfg, sms, at, stream):
         latest = _arr(info, 4 * self.world, np.int64).reshape(self.world, 4)[:, 2]
         c0 = self.clock
         live = latest[latest != -(1 << 63)]

@@ -70,10 +70,11 @@ def test_route_kernels_match_restatement(rl, world):
         outs = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
                [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
                 torch.empty(m, dtype=torch.int32, device="cuda")]
-        r.merge(m, send.data_ptr(), info.cuda().data_ptr(), *[x.data_ptr() for x in outs], s)
+        info_d = info.cuda()
+        r.merge(m, send.data_ptr(), info_d.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs], s)
         outs_h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
                  [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
-        ops.merge(m, send_h.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs_h], None)
+        ops.merge(m, send_h.data_ptr(), info.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs_h], None)
         assert r.sync(s) == rl.RL_OK
         for a, b in zip(outs, outs_h):
             assert torch.equal(a.cpu(), b)
@@ -118,9 +119,9 @@ def test_merge_single_sorted_source_keeps_order(rl):
         h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
             [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
         rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
-        r.merge(m, rt.data_ptr(), it.data_ptr(), *[x.data_ptr() for x in d], s)
+        r.merge(m, rt.data_ptr(), it.data_ptr(), torch.from_numpy(info).data_ptr(), *[x.data_ptr() for x in d], s)
         rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
-        ops.merge(m, rh.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
+        ops.merge(m, rh.data_ptr(), ih.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
         assert r.sync(s) == rl.RL_OK
         for a, b in zip(d, h):
             assert torch.equal(a.cpu(), b)
@@ -153,9 +154,9 @@ def test_merge_wide_time_spans_and_unsorted_sources(rl, span_bits):
     h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
         [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
     rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
-    r.merge(m, rt.data_ptr(), it.data_ptr(), *[x.data_ptr() for x in d], s)
+    r.merge(m, rt.data_ptr(), it.data_ptr(), torch.from_numpy(info).data_ptr(), *[x.data_ptr() for x in d], s)
     rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
-    ops.merge(m, rh.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
+    ops.merge(m, rh.data_ptr(), ih.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
     assert r.sync(s) == rl.RL_OK
     for a, b in zip(d, h):
         assert torch.equal(a.cpu(), b)
@@ -173,8 +174,9 @@ def test_merge_reports_a_too_wide_time_span(rl):
            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
             torch.empty(m, dtype=torch.int32, device="cuda")]
     s = torch.cuda.current_stream().cuda_stream
-    info = torch.tensor([[m - 100, T0, T0 + (1 << 49), 0], [100, T0, T0, 1]], dtype=torch.int64, device="cuda")
-    r.merge(m, rec.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs], s)
+    info_h = torch.tensor([[m - 100, T0, T0 + (1 << 49), 0], [100, T0, T0, 1]], dtype=torch.int64)
+    info = info_h.cuda()
+    r.merge(m, rec.data_ptr(), info.data_ptr(), info_h.data_ptr(), *[x.data_ptr() for x in outs], s)
     assert r.sync(s) == rl.RL_EINVAL
     r.close()
 
