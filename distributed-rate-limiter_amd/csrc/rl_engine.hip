@@ -115,7 +115,8 @@ __device__ inline uint32_t probe_request(uint64_t k, uint32_t c, int64_t nn, con
 }
 
 // find-or-insert every request's key; sort key = global slot id; fused
-// per-pass digit histograms (LDS, then one global atomic per bin per block).
+// per-pass digit histograms (LDS, then one global atomic per bin per block);
+// pass p's digit is 8 bits at shift (shifts >> 8p) & 31 (see sort_shifts).
 // Each thread takes PROBE_R requests and issues their loads phase by phase
 // (inputs, then every first table probe) before resolving any: the kernel is
 // latency-bound on random table reads, and this keeps PROBE_R of them in
@@ -125,8 +126,8 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     uint32_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ n,
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
     uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
-    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, ReqArgs a, ReqRec<XS>* __restrict__ rec,
-    uint32_t* eflags) {
+    uint32_t* __restrict__ sk, uint32_t* ghist, int passes, uint32_t shifts, ReqArgs a,
+    ReqRec<XS>* __restrict__ rec, uint32_t* eflags) {
     __shared__ uint32_t lh[4][RADIX];
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
@@ -171,7 +172,8 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             // one record per request: k_permute's sorted-order gather then
             // touches one line fragment instead of four arrays
             rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r]);
-            for (int p = 0; p < passes; p++) atomicAdd(&lh[p][(slot >> (8 * p)) & (RADIX - 1)], 1u);
+            for (int p = 0; p < passes; p++)
+                atomicAdd(&lh[p][(slot >> ((shifts >> (8 * p)) & 31u)) & (RADIX - 1)], 1u);
         }
     }
     if (ef) atomicOr(eflags, ef);
@@ -386,7 +388,21 @@ constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iter
                                                // [8..19] timers [20] exact tiles [21] serial steps
 constexpr uint32_t CTRL_DBGN = 88;
 constexpr uint32_t CTRL_UPB = CTRL_DBG + CTRL_DBGN;   // [UP_NB] bucket fill counters (k_unpermute_bucket)
-constexpr uint32_t CTRL_WORDS = CTRL_UPB + UP_NB;
+constexpr uint32_t CTRL_PLAN = CTRL_UPB + UP_NB;      // [0] every MSD bucket fits k_sort_local [1] it does not
+constexpr uint32_t CTRL_WORDS = CTRL_PLAN + 2;
+
+// The grouping sort's digits.  One pass: bits [0, 8).  More: the MSD pass
+// first, the top 8 bits [B - 8, B) of the B-bit slot ids, then either one
+// k_sort_local over the buckets (each sorted in LDS by the bits below B - 8)
+// or, when a bucket is too large for it (a hot key), the LSD passes at
+// 0, 8, ... over bits [0, B - 8).  Every pass is stable and the digits cover
+// every bit, so either way equal slots end up contiguous in arrival order.
+static uint32_t sort_shifts(int bits, int passes) {
+    if (passes <= 1) return 0u;
+    uint32_t sh = (uint32_t)(bits - 8);
+    for (int p = 1; p < passes; p++) sh |= (uint32_t)(8 * (p - 1)) << (8 * p);
+    return sh;
+}
 
 uint64_t pow2_at_least(uint64_t v) {
     uint64_t p = 1;
@@ -460,6 +476,7 @@ struct rl_engine {
     Spill spill() const { return Spill{d_spill, spill_cap - 1}; }
     uint32_t win_base = 0, invalid_key = 0;
     int sort_bits = 0, sort_passes = 0;
+    uint32_t sort_shifts = 0;   // digit shift of each histogram / pass (8 bits each; sort_shifts())
 
     uint32_t max_batch = 0;
     uint32_t max_tiles = 0;
@@ -651,6 +668,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     e->invalid_key = (uint32_t)(e->tb_cap + e->win_cap);
     e->sort_bits = bitlen(e->invalid_key);
     e->sort_passes = (e->sort_bits + 7) / 8;
+    e->sort_shifts = sort_shifts(e->sort_bits, e->sort_passes);
     e->max_batch = o->max_batch;
     e->max_tiles = (o->max_batch + SORT_TILE - 1) / SORT_TILE;
 
@@ -887,26 +905,46 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (xs)
         k_probe<1, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
-            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, a,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, e->sort_shifts, a,
             static_cast<ReqRec<true>*>(B.rec), e->d_eflags);
     else
         k_probe<1, false><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
-            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, a,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, e->sort_shifts, a,
             static_cast<ReqRec<false>*>(B.rec), e->d_eflags);
     if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
-    for (int p = 0; p < e->sort_passes; p++) {
-        uint32_t* status = B.status + (size_t)p * e->max_tiles * RADIX;
-        if (p == 0)
-            k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
-                                                           status, B.ctrl + CTRL_TILE + p, e->d_eflags);
-        else
-            k_sort_pass<false><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * p, ghist + p * RADIX,
-                                                            status, B.ctrl + CTRL_TILE + p, e->d_eflags);
-        std::swap(kin, kout);
-        std::swap(vin, vout);
+    const int P = e->sort_passes;
+    if (P <= 1) {
+        k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
+                                                       B.ctrl + CTRL_TILE, e->d_eflags);
+        kin = B.sk1;
+        vin = B.sv1;
+    } else {
+        // MSD pass (and the plan: every bucket fits LDS or not), then either
+        // k_sort_local or the LSD passes over the lower bits; both end in
+        // the same buffers
+        uint32_t* plan = B.ctrl + CTRL_PLAN;
+        k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(B.sk0, B.sv0, B.sk1, B.sv1, m, e->sort_bits - 8, ghist,
+                                                       B.status, B.ctrl + CTRL_TILE, e->d_eflags, nullptr, plan,
+                                                       LOC_MAX);
+        const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
+        uint32_t* fk = odd ? B.sk0 : B.sk1;
+        uint32_t* fv = odd ? B.sv0 : B.sv1;
+        k_sort_local<<<RADIX, LOC_BLOCK, 0, f>>>(B.sk1, B.sv1, fk, fv, ghist, P - 1, plan + 1);
+        kin = B.sk1;
+        vin = B.sv1;
+        kout = B.sk0;
+        vout = B.sv0;
+        for (int p = 1; p < P; p++) {
+            uint32_t* status = B.status + (size_t)p * e->max_tiles * RADIX;
+            k_sort_pass<false><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * (p - 1), ghist + p * RADIX,
+                                                            status, B.ctrl + CTRL_TILE + p, e->d_eflags, plan);
+            std::swap(kin, kout);
+            std::swap(vin, vout);
+        }
+        // kin / vin == fk / fv
     }
     if (tall) (void)hipEventRecord(ev[2], f);
     // sorted keys/values are now in kin/vin
@@ -1259,6 +1297,7 @@ extern "C" int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, u
     e->invalid_key = (uint32_t)(tb_cap + win_cap);
     e->sort_bits = bitlen(e->invalid_key);
     e->sort_passes = (e->sort_bits + 7) / 8;
+    e->sort_shifts = sort_shifts(e->sort_bits, e->sort_passes);
     e->stats.sort_bits = e->sort_bits;
     e->stats.sort_passes = e->sort_passes;
     return out ? rl_table_info_get(e, now_ms, out) : RL_OK;

@@ -190,6 +190,29 @@ def test_segment_tile_boundaries(rl, counts):
     run_both(rl, 0, configs, split((key, ts, n, cfg, None), [m]))
 
 
+@pytest.mark.parametrize("counts", [
+    [12_288, 5000, 3000, 1, 2],        # every MSD bucket fits LDS (12288): k_sort_local
+    [12_289, 7, 9000, 4096],           # one key just past it: the LSD passes
+    [20_000, 4000, 4000, 1, 64],       # a hot key: the LSD passes
+])
+def test_sort_local_and_lsd_paths(rl, counts):
+    # the grouping sort's MSD pass picks k_sort_local when every bucket of its
+    # digit fits LDS and the LSD passes otherwise; both must group every key's
+    # requests in arrival order (tables of 2^16: 18-bit slot ids, 3 passes)
+    configs = CONFIG_SETS["mixed"]
+    rng = np.random.default_rng(sum(counts))
+    key = np.concatenate([np.full(c, 77 + i, np.uint64) for i, c in enumerate(counts)])
+    extra = rng.integers(1000, 60_000, 30_000).astype(np.uint64)    # many light keys around them
+    key = np.concatenate([key, extra])[rng.permutation(key.size + extra.size)]
+    m = key.size
+    ts = T0 + np.cumsum(rng.integers(0, 300_000, m)).astype(np.int64)
+    n = rng.choice([1, 1, 2], m).astype(np.int64)
+    n[rng.random(m) < 0.003] = 0
+    cfg = (key % len(configs)).astype(np.uint32)
+    for profile in (0, 1):
+        run_both(rl, profile, configs, split((key, ts, n, cfg, None), [m]), tb=1 << 16, win=1 << 16)
+
+
 def test_single_hot_key_full_batch(rl):
     # the bench's diagnostic workload: one key carries the whole 1M batch
     g = traces.TokenBucketZipf(nkeys=1, batch=1_000_000)
