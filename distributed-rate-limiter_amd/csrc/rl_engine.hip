@@ -916,6 +916,9 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
     const int P = e->sort_passes;
+    uint32_t* segctr = B.ctrl + CTRL_NSEG;
+    const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
+    const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
     if (P <= 1) {
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
                                                        B.ctrl + CTRL_TILE, e->d_eflags);
@@ -932,7 +935,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
         uint32_t* fk = odd ? B.sk0 : B.sk1;
         uint32_t* fv = odd ? B.sv0 : B.sv1;
-        k_sort_local<<<RADIX, LOC_BLOCK, 0, f>>>(B.sk1, B.sv1, fk, fv, ghist, P - 1, plan + 1);
+        k_sort_local<<<RADIX, LOC_BLOCK, 0, f>>>(B.sk1, B.sv1, fk, fv, ghist, e->sort_bits - 8, plan + 1,
+                                                 e->invalid_key, e->win_base, e->heavy_min, huge_min, lists);
         kin = B.sk1;
         vin = B.sv1;
         kout = B.sk0;
@@ -948,11 +952,9 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     }
     if (tall) (void)hipEventRecord(ev[2], f);
     // sorted keys/values are now in kin/vin
-    uint32_t* segctr = B.ctrl + CTRL_NSEG;
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
-    const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
-    k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min,
-                                      std::max(e->huge_min, e->heavy_min), lists);
+    k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min, huge_min, lists,
+                                             P > 1 ? B.ctrl + CTRL_PLAN : nullptr);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     // (the server clock only when the caller gave one: else floor(ts / 1e6) where it is read)
     ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, nullptr, nullptr, nullptr,

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rl_semantics.h"
+#include "rl_sort.h"
 #include "rl_table.h"
 #include "rl_window.h"
 
@@ -407,7 +408,8 @@ __device__ inline uint32_t seg_skew(uint32_t i) { return i + (i >> 4); }   // LD
 
 __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ sk, uint32_t m,
                                                   uint32_t invalid_key, uint32_t win_base, uint32_t heavy_min,
-                                                  uint32_t huge_min, SegLists L) {
+                                                  uint32_t huge_min, SegLists L, const uint32_t* skip) {
+    if (skip && *skip) return;   // k_sort_local built the lists
     __shared__ uint32_t s_k[SEG_TILE + SEG_TILE / 16];
     __shared__ uint32_t s_next[256];      // first head of chunk t, then of chunks > t
     __shared__ uint32_t s_cnt[4], s_base[4], s_open, s_open_end;
@@ -513,6 +515,219 @@ __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ s
             L.list[which][s_base[which] + off] = rec[q];
         }
         __syncthreads();
+    }
+}
+
+// The grouping sort's second half when every bucket of the MSD pass fits
+// LDS (rl_engine.hip sort_shifts): one block per bucket -- the elements whose
+// slot id has the MSD digit blockIdx.x, contiguous and in arrival order after
+// the MSD pass -- sorts it by the `low_bits` bits below the digit with stable
+// passes entirely in LDS (8 bits a pass, the last one narrower; the ranking of
+// k_sort_pass: ballots per wave, digit counts per wave, a scan over (digit,
+// wave)) and writes it to the same range of kout / vout (which may alias kin
+// / vin: the bucket is read before anything is written).  Equal slots share
+// a bucket, so this groups every key with its requests in arrival order like
+// the LSD passes it replaces, and a key's segment never leaves its bucket:
+// the block also builds the segment work lists k_segments would (same lists,
+// same classes; heads in position order inside the block).  skip: the MSD
+// pass found a bucket too large (the LSD passes and k_segments run instead).
+constexpr int LOC_BLOCK = 1024;
+constexpr int LOC_ITEMS = 12;
+constexpr uint32_t LOC_MAX = LOC_BLOCK * LOC_ITEMS;   // 12288 elements per bucket
+constexpr int LOC_WAVES = LOC_BLOCK / 64;
+
+__global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
+                                                          uint32_t* vout, const uint32_t* __restrict__ ghist_msd,
+                                                          int low_bits, const uint32_t* skip, uint32_t invalid_key,
+                                                          uint32_t win_base, uint32_t heavy_min, uint32_t huge_min,
+                                                          SegLists L) {
+    if (*skip) return;
+    __shared__ uint32_t s_k[LOC_MAX], s_v[LOC_MAX];
+    __shared__ uint32_t s_cnt[LOC_WAVES][RADIX];
+    __shared__ uint32_t s_base[RADIX];
+    __shared__ uint32_t s_w[LOC_WAVES][4];
+    __shared__ uint32_t s_lbase[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t cnt = ghist_msd[b];
+    if (cnt == 0) return;
+    // the bucket's range: exclusive prefix of the MSD histogram up to b
+    uint32_t pre = (uint32_t)tid < b ? ghist_msd[tid] : 0u;
+    for (int off = 32; off > 0; off >>= 1) pre += __shfl_xor(pre, off);
+    if (lane == 0 && wave < 4) s_w[wave][0] = pre;
+    __syncthreads();
+    const uint32_t start = s_w[0][0] + s_w[1][0] + s_w[2][0] + s_w[3][0];
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t base = (uint32_t)wave * (64 * LOC_ITEMS);
+    // element e = base + 64 j + lane of the bucket, straight from HBM
+    uint32_t key[LOC_ITEMS], val[LOC_ITEMS], rank[LOC_ITEMS];
+#pragma unroll
+    for (int j = 0; j < LOC_ITEMS; j++) {
+        const uint32_t e = base + j * 64 + lane;
+        const bool ok = e < cnt;
+        key[j] = ok ? kin[start + e] : 0u;
+        val[j] = ok ? vin[start + e] : 0u;
+    }
+    for (int shift = 0; shift < low_bits; shift += 8) {
+        const int bits = low_bits - shift < 8 ? low_bits - shift : 8;
+        for (int d = tid; d < LOC_WAVES * RADIX; d += LOC_BLOCK) (&s_cnt[0][0])[d] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            const uint32_t e = base + j * 64 + lane;
+            const bool ok = e < cnt;
+            const uint32_t d = (key[j] >> shift) & ((1u << bits) - 1u);
+            uint64_t peers = __ballot(ok);
+            for (int bt = 0; bt < bits; bt++) {
+                const uint32_t bit = (d >> bt) & 1u;
+                const uint64_t bb = __ballot(bit);
+                peers &= bit ? bb : ~bb;
+            }
+            if (ok) {
+                const uint32_t below = __popcll(peers & lt);
+                const uint32_t cur = s_cnt[wave][d];
+                rank[j] = cur + below;
+                if (below == 0) s_cnt[wave][d] = cur + (uint32_t)__popcll(peers);
+            }
+        }
+        __syncthreads();
+        // per digit: exclusive prefix over the waves; digit totals scanned
+        uint32_t tot = 0;
+        if (tid < RADIX) {
+            for (int w = 0; w < LOC_WAVES; w++) {
+                const uint32_t c = s_cnt[w][tid];
+                s_cnt[w][tid] = tot;
+                tot += c;
+            }
+        }
+        uint32_t inc = tot;
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += t;
+        }
+        if (tid < RADIX && lane == 63) s_w[wave][0] = inc;
+        __syncthreads();
+        if (tid < RADIX) {
+            uint32_t wp = 0;
+            for (int w = 0; w < wave; w++) wp += s_w[w][0];
+            s_base[tid] = wp + inc - tot;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            const uint32_t e = base + j * 64 + lane;
+            if (e < cnt) {
+                const uint32_t d = (key[j] >> shift) & ((1u << bits) - 1u);
+                const uint32_t pos = s_base[d] + s_cnt[wave][d] + rank[j];
+                s_k[pos] = key[j];
+                s_v[pos] = val[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {   // the next pass's elements, in the new order
+            const uint32_t e = base + j * 64 + lane;
+            key[j] = e < cnt ? s_k[e] : 0u;
+            val[j] = e < cnt ? s_v[e] : 0u;
+        }
+    }
+    if (low_bits <= 0) {   // (never: the MSD digit is the top 8 of >= 12 bits) keep s_k valid
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            const uint32_t e = base + j * 64 + lane;
+            if (e < cnt) s_k[e] = key[j];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < LOC_ITEMS; j++) {
+        const uint32_t e = base + j * 64 + lane;
+        if (e < cnt) {
+            kout[start + e] = key[j];
+            vout[start + e] = val[j];
+        }
+    }
+    // ---- segments of the bucket (k_segments' lists) ----
+    // boundaries in position order: a head (a valid key unlike its
+    // predecessor) or an invalid key (rejected requests end a segment); the
+    // compacted boundary positions go to s_v (no longer needed)
+    uint32_t bnd[LOC_ITEMS];
+    uint32_t run = 0;   // boundaries of this wave so far
+#pragma unroll
+    for (int j = 0; j < LOC_ITEMS; j++) {
+        const uint32_t e = base + j * 64 + lane;
+        const bool ok = e < cnt;
+        const bool valid = ok && key[j] != invalid_key;
+        const bool head = valid && (e == 0 || s_k[e - 1] != key[j]);
+        const bool bd = head || (ok && !valid);
+        const uint64_t bm = __ballot(bd);
+        bnd[j] = bd ? run + (uint32_t)__popcll(bm & lt) : 0xffffffffu;
+        rank[j] = head ? 1u : 0u;
+        run += (uint32_t)__popcll(bm);
+    }
+    if (lane == 0) s_w[wave][0] = run;
+    __syncthreads();
+    uint32_t wpre = 0, nb = 0;
+    for (int w = 0; w < LOC_WAVES; w++) {
+        const uint32_t c = s_w[w][0];
+        wpre += w < wave ? c : 0u;
+        nb += c;
+    }
+#pragma unroll
+    for (int j = 0; j < LOC_ITEMS; j++) {
+        if (bnd[j] != 0xffffffffu) {
+            bnd[j] += wpre;
+            s_v[bnd[j]] = base + j * 64 + lane;
+        }
+    }
+    __syncthreads();
+    // each head: its end (the next boundary, or the bucket end), its list,
+    // and its slot in the list (position order: per list a wave ballot rank,
+    // then the waves before, then the block's base from one atomic per list)
+    uint32_t which[LOC_ITEMS], len[LOC_ITEMS];
+    uint32_t lrun[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < LOC_ITEMS; j++) {
+        which[j] = 4u;
+        len[j] = 0u;
+        if (rank[j]) {
+            const uint32_t e = base + j * 64 + lane;
+            const uint32_t end = bnd[j] + 1 < nb ? s_v[bnd[j] + 1] : cnt;
+            len[j] = end - e;
+            const bool tb = key[j] < win_base;
+            which[j] = len[j] < heavy_min ? 1u : !tb ? 2u : len[j] >= huge_min ? 3u : 0u;
+        }
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            const uint64_t wm = __ballot(which[j] == (uint32_t)w);
+            if (which[j] == (uint32_t)w) bnd[j] = lrun[w] + (uint32_t)__popcll(wm & lt);
+            lrun[w] += (uint32_t)__popcll(wm);
+        }
+    }
+    __syncthreads();   // s_w reused
+    if (lane == 0)
+        for (int w = 0; w < 4; w++) s_w[wave][w] = lrun[w];
+    __syncthreads();
+    if (tid < 4) {
+        uint32_t t = 0;
+        for (int w = 0; w < LOC_WAVES; w++) t += s_w[w][tid];
+        s_lbase[tid] = t ? atomicAdd(&L.count[tid], t) : 0u;
+    }
+    __syncthreads();
+    uint32_t wb[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        uint32_t x = s_lbase[w];
+        for (int v = 0; v < wave; v++) x += s_w[v][w];
+        wb[w] = x;
+    }
+#pragma unroll
+    for (int j = 0; j < LOC_ITEMS; j++) {
+        if (which[j] < 4u) {
+            const uint32_t w = which[j];
+            const uint32_t at = (w == 0 ? wb[0] : w == 1 ? wb[1] : w == 2 ? wb[2] : wb[3]) + bnd[j];
+            L.list[w][at] = SegRec{start + base + j * 64 + lane, len[j]};
+        }
     }
 }
 

@@ -184,117 +184,4 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     }
 }
 
-// The grouping sort's second half when every bucket of the MSD pass fits
-// LDS: one block per bucket (the elements whose digit at msd_shift is
-// blockIdx.x, contiguous and in arrival order after the MSD pass) sorts it by
-// the bits below msd_shift with `npass` stable 8-bit passes entirely in LDS
-// (the ranking of k_sort_pass: ballots per wave, digit counts per wave, a
-// scan over (digit, wave)), and writes it to the same range of kout/vout
-// (which may alias kin/vin: the bucket is staged in LDS first).  Equal keys
-// share a bucket, so the result groups every key with its requests in
-// arrival order, like the LSD passes it replaces.  skip: the MSD pass found
-// a bucket too large (the global LSD passes run instead).
-constexpr int LOC_BLOCK = 1024;
-constexpr int LOC_ITEMS = 12;
-constexpr uint32_t LOC_MAX = LOC_BLOCK * LOC_ITEMS;   // 12288 elements per bucket
-constexpr int LOC_WAVES = LOC_BLOCK / 64;
-
-static __global__ __attribute__((unused)) __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
-                                                          uint32_t* vout, const uint32_t* __restrict__ ghist_msd,
-                                                          int npass, const uint32_t* skip) {
-    if (*skip) return;
-    __shared__ uint32_t s_k[LOC_MAX], s_v[LOC_MAX];
-    __shared__ uint32_t s_cnt[LOC_WAVES][RADIX];
-    __shared__ uint32_t s_base[RADIX];
-    __shared__ uint32_t s_w[4];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t b = blockIdx.x;
-    // the bucket's range: exclusive prefix of the MSD histogram up to b
-    uint32_t pre = 0;
-    for (uint32_t d = (uint32_t)tid; d < b; d += LOC_BLOCK) pre += ghist_msd[d];
-    for (int off = 32; off > 0; off >>= 1) pre += __shfl_xor(pre, off);
-    if (lane == 0 && wave < 4) s_w[wave] = pre;
-    __syncthreads();
-    const uint32_t start = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    const uint32_t cnt = ghist_msd[b];
-    if (cnt == 0) return;
-    for (uint32_t i = tid; i < cnt; i += LOC_BLOCK) {
-        s_k[i] = kin[start + i];
-        s_v[i] = vin[start + i];
-    }
-    __syncthreads();
-    const uint64_t lt = (1ull << lane) - 1ull;
-    const uint32_t base = (uint32_t)wave * (64 * LOC_ITEMS);
-    for (int p = 0; p < npass && cnt > 1; p++) {
-        const int shift = 8 * p;
-        uint32_t key[LOC_ITEMS], val[LOC_ITEMS], rank[LOC_ITEMS];
-#pragma unroll
-        for (int j = 0; j < LOC_ITEMS; j++) {
-            const uint32_t e = base + j * 64 + lane;
-            const bool ok = e < cnt;
-            key[j] = ok ? s_k[e] : 0u;
-            val[j] = ok ? s_v[e] : 0u;
-        }
-        for (int d = tid; d < LOC_WAVES * RADIX; d += LOC_BLOCK) (&s_cnt[0][0])[d] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < LOC_ITEMS; j++) {
-            const uint32_t e = base + j * 64 + lane;
-            const bool ok = e < cnt;
-            const uint32_t d = (key[j] >> shift) & (RADIX - 1);
-            uint64_t peers = __ballot(ok);
-#pragma unroll
-            for (int bt = 0; bt < 8; bt++) {
-                const uint32_t bit = (d >> bt) & 1u;
-                const uint64_t bb = __ballot(bit);
-                peers &= bit ? bb : ~bb;
-            }
-            if (ok) {
-                const uint32_t below = __popcll(peers & lt);
-                const uint32_t cur = s_cnt[wave][d];
-                rank[j] = cur + below;
-                if (below == 0) s_cnt[wave][d] = cur + (uint32_t)__popcll(peers);
-            }
-        }
-        __syncthreads();
-        // per digit: exclusive prefix over the waves; digit totals scanned
-        uint32_t tot = 0;
-        if (tid < RADIX) {
-            for (int w = 0; w < LOC_WAVES; w++) {
-                const uint32_t c = s_cnt[w][tid];
-                s_cnt[w][tid] = tot;
-                tot += c;
-            }
-        }
-        uint32_t inc = tot;
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t t = __shfl_up(inc, off, 64);
-            if (lane >= off) inc += t;
-        }
-        if (tid < RADIX && lane == 63) s_w[wave] = inc;
-        __syncthreads();
-        if (tid < RADIX) {
-            uint32_t wp = 0;
-            for (int w = 0; w < wave; w++) wp += s_w[w];
-            s_base[tid] = wp + inc - tot;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < LOC_ITEMS; j++) {
-            const uint32_t e = base + j * 64 + lane;
-            if (e < cnt) {
-                const uint32_t d = (key[j] >> shift) & (RADIX - 1);
-                const uint32_t pos = s_base[d] + s_cnt[wave][d] + rank[j];
-                s_k[pos] = key[j];
-                s_v[pos] = val[j];
-            }
-        }
-        __syncthreads();
-    }
-    for (uint32_t i = tid; i < cnt; i += LOC_BLOCK) {
-        kout[start + i] = s_k[i];
-        vout[start + i] = s_v[i];
-    }
-}
-
 }  // namespace rl
