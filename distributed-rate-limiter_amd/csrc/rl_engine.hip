@@ -504,6 +504,8 @@ struct rl_engine {
     // GROUP_LDS bytes at least) then never share a CU with a chain
     size_t chain_pad[2] = {0, 0};
     uint32_t* d_eflags = nullptr;
+    unsigned long long* d_count = nullptr;   // table counts / GC counters (rl_table_info_get, rl_table_gc)
+    unsigned long long* h_count = nullptr;   // pinned host copy
     uint32_t* stamp_ring = nullptr;   // RL_STAMP_KERNELS diagnostics
 
     // host-API staging (device side)
@@ -617,6 +619,8 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_spill);
     for (auto& B : e->set) free_set(B);
     (void)hipFree(e->d_eflags);
+    (void)hipFree(e->d_count);
+    if (e->h_count) (void)hipHostFree(e->h_count);
     (void)hipFree(e->stamp_ring);
     (void)hipFree(e->small_kid);
     (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
@@ -712,6 +716,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_spill, sizeof(SpillEntry) * e->spill_cap) == hipSuccess;
     for (auto& B : e->set) ok = ok && alloc_set(B, M, e->zero_bytes, status_words);
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
+    ok &= hipMalloc(&e->d_count, 8 * sizeof(unsigned long long)) == hipSuccess;
+    ok &= hipHostMalloc(&e->h_count, 8 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess;
     ok &= hipMalloc(&e->d_key, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_ts, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_n, 8 * M) == hipSuccess;
@@ -1067,6 +1073,16 @@ static int warm_up(rl_engine* e) {
         const int r = run_batch(e, mb, ax, s, false);
         if (r != RL_OK) return r;
     }
+    // the table count / GC / key listing kernels, on empty ranges: a server's
+    // first periodic count must not wait for their lazy load
+    k_table_count<<<1, 256, 0, s>>>(e->d_tb, 0, 0, e->profile, e->d_count);
+    k_table_count<<<1, 256, 0, s>>>(e->d_win, 0, 0, e->profile, e->d_count);
+    k_table_count<<<1, 256, 0, s>>>(e->d_spill, 0, 0, e->profile, e->d_count);
+    k_rehash<<<1, 256, 0, s>>>(e->d_tb, 0, e->d_tb, e->tb_cap - 1, 0, e->profile, e->d_count);
+    k_rehash<<<1, 256, 0, s>>>(e->d_win, 0, e->d_win, e->win_cap - 1, 0, e->profile, e->d_count);
+    k_spill_rehash<<<1, 256, 0, s>>>(e->d_spill, 0, e->d_spill, e->spill_cap - 1, e->d_win, e->win_cap - 1, 0,
+                                     e->profile, e->d_count);
+    HIPCHK(e, hipGetLastError());
     const int r = drain(e);
     if (r != RL_OK) return r;
     HIPCHK(e, hipMemset(e->d_eflags, 0, 4));
@@ -1198,17 +1214,17 @@ extern "C" int rl_table_info_get(rl_engine* e, int64_t now_ms, rl_table_info* ou
     (void)hipSetDevice(e->device);
     int r = drain(e);
     if (r != RL_OK) return r;
-    unsigned long long* d = nullptr;
-    HIPCHK(e, hipMalloc(&d, 6 * sizeof(unsigned long long)));
-    unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
+    // preallocated counters (no hipMalloc / hipFree, which synchronize the
+    // device, on a server's periodic count)
+    unsigned long long* d = e->d_count;
+    unsigned long long* h = e->h_count;
     hipStream_t s = e->stream;
-    bool ok = hipMemsetAsync(d, 0, sizeof h, s) == hipSuccess;
+    bool ok = hipMemsetAsync(d, 0, 6 * sizeof(unsigned long long), s) == hipSuccess;
     k_table_count<<<1024, 256, 0, s>>>(e->d_tb, e->tb_cap, now_ms, e->profile, d);
     k_table_count<<<1024, 256, 0, s>>>(e->d_win, e->win_cap, now_ms, e->profile, d + 2);
     k_table_count<<<1024, 256, 0, s>>>(e->d_spill, e->spill_cap, now_ms, e->profile, d + 4);
-    ok = ok && hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, s) == hipSuccess;
+    ok = ok && hipMemcpyAsync(h, d, 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s) == hipSuccess;
     ok = ok && hipStreamSynchronize(s) == hipSuccess;
-    (void)hipFree(d);
     if (!ok) return fail(e, RL_EDEVICE, "table count failed");
     return copy_out(out, rl_table_info{sizeof(rl_table_info), 0, e->tb_cap, h[0], h[1], e->win_cap, h[2], h[3],
                                        e->spill_cap, h[4], h[5]});
