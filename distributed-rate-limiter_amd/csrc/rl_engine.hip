@@ -811,6 +811,11 @@ extern "C" int rl_config_register(rl_engine* e, uint8_t alg, int64_t limit, int6
     return RL_OK;
 }
 
+extern "C" int rl_config_table(rl_engine* e, uint32_t cfg_id) {
+    if (!e || cfg_id >= e->h_cfg.size()) return RL_EINVAL;
+    return e->h_cfg[cfg_id].alg == ALG_TOKEN_BUCKET ? 0 : 1;
+}
+
 static hipEvent_t take_event(rl_engine* e) {
     if (!e->ev_pool.empty()) {
         hipEvent_t ev = e->ev_pool.back();

@@ -163,6 +163,16 @@ public:
         (void)hipSetDevice(dev_id_);
         return rl_table_gc(e_, now_ms, tb_cap, win_cap, out);
     }
+    int table_of(uint32_t cfg) override {
+        if (cfg >= table_.size()) {      // configs registered since: look them up once
+            for (uint32_t c = (uint32_t)table_.size();; c++) {
+                const int t = rl_config_table(e_, c);
+                if (t < 0) break;
+                table_.push_back((int8_t)t);
+            }
+        }
+        return cfg < table_.size() ? table_[cfg] : -1;
+    }
 
 private:
     struct Dev {
@@ -183,6 +193,7 @@ private:
         s.dec = q + 24 * M;
     }
     rl_engine* e_;
+    std::vector<int8_t> table_;  // table_of per config id (submitter thread)
     int dev_id_ = 0;             // the engine's device: current when the coalescer is created
     // batches up to this size run zero-copy on the pinned slot (larger ones:
     // one H2D copy, device-resident inputs for the grouping's several reads)
@@ -525,7 +536,22 @@ int Coalescer::run_table_op(Sub* op) {
 void Coalescer::auto_gc(const Slot& s) {
     if (o_.gc_interval_ns <= 0 || s.m == 0) return;
     const int64_t now = steady_ns();
-    if (gc_counted_ && gc_launched_ + s.m <= gc_budget_ && now - gc_last_check_ < o_.gc_interval_ns) return;
+    // the batch's requests per table: a token-bucket request can insert one
+    // entry into the token-bucket table, a window request one into the window
+    // table and one into the spill table; a request of an unknown config counts
+    // for both
+    uint64_t mt[2] = {0, 0};
+    for (size_t i = 0; i < s.m; i++) {
+        const int t = be_->table_of(s.cfg[i]);
+        if (t != 1) mt[0]++;
+        if (t != 0) mt[1]++;
+    }
+    if (gc_counted_ && gc_launched_[0] + mt[0] <= gc_budget_[0] && gc_launched_[1] + mt[1] <= gc_budget_[1] &&
+        now - gc_last_check_ < o_.gc_interval_ns) {
+        gc_launched_[0] += mt[0];
+        gc_launched_[1] += mt[1];
+        return;
+    }
     // server clock of the GC: no later request may carry an older one (the
     // engine's clock is floor(ts / 1e6)); requests come in near time order,
     // within gc_margin_ms of each other
@@ -536,20 +562,21 @@ void Coalescer::auto_gc(const Slot& s) {
     in.struct_size = sizeof in;
     if (be_->table_info(now_ms, &in) != RL_OK) {
         gc_counted_ = true;
-        gc_budget_ = 0;
+        gc_budget_[0] = gc_budget_[1] = 0;
         gc_last_check_ = now;
-        gc_launched_ = 0;
+        gc_launched_[0] = mt[0];
+        gc_launched_[1] = mt[1];
         return;
     }
     const double hi = o_.gc_high_pct / 100.0;
     auto high = [&](uint64_t cap) { return (uint64_t)(hi * (double)cap); };
-    auto full = [&](uint64_t used, uint64_t cap) { return used + s.m > high(cap); };
+    auto full = [&](uint64_t used, uint64_t cap, uint64_t m) { return used + m > high(cap); };
     {
         std::lock_guard<std::mutex> g(mu_);
         st_.gc_checks++;
     }
-    if (full(in.tb_used, in.tb_capacity) || full(in.win_used, in.win_capacity) ||
-        full(in.spill_used, in.spill_capacity)) {
+    if (full(in.tb_used, in.tb_capacity, mt[0]) || full(in.win_used, in.win_capacity, mt[1]) ||
+        full(in.spill_used, in.spill_capacity, mt[1])) {
         // grow a table whose live keys alone fill half its headroom
         auto grow = [&](uint64_t live, uint64_t cap, uint64_t lim) -> uint64_t {
             if (live <= high(cap) / 2) return 0;
@@ -574,11 +601,12 @@ void Coalescer::auto_gc(const Slot& s) {
         if (ok) in = out;
     }
     auto room = [&](uint64_t used, uint64_t cap) -> uint64_t { return used < high(cap) ? high(cap) - used : 0; };
-    gc_budget_ = std::min({room(in.tb_used, in.tb_capacity), room(in.win_used, in.win_capacity),
-                           room(in.spill_used, in.spill_capacity)});
+    gc_budget_[0] = room(in.tb_used, in.tb_capacity);
+    gc_budget_[1] = std::min(room(in.win_used, in.win_capacity), room(in.spill_used, in.spill_capacity));
     gc_counted_ = true;
     gc_last_check_ = now;
-    gc_launched_ = 0;
+    gc_launched_[0] = mt[0];      // this batch launches after the count
+    gc_launched_[1] = mt[1];
 }
 
 void Coalescer::submitter() {
@@ -692,7 +720,6 @@ void Coalescer::submitter() {
             }
             s.m = m;
             auto_gc(s);
-            gc_launched_ += m;
             s.status = be_->launch(si, s);
         }
         if (trace_cap_) s.t_launched = steady_ns();

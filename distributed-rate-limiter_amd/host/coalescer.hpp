@@ -58,6 +58,9 @@ public:
     // synchronous table operations (the GPU engine drains its batches first)
     virtual int table_info(int64_t now_ms, rl_table_info* out) = 0;
     virtual int gc(int64_t now_ms, uint64_t tb_cap, uint64_t win_cap, rl_table_info* out) = 0;
+    // the table a config's keys live in (0 token bucket, 1 window), or -1
+    // when unknown (the automatic GC then counts the request against both)
+    virtual int table_of(uint32_t cfg) { (void)cfg; return -1; }
 };
 
 std::unique_ptr<Backend> make_gpu_backend(rl_engine* e);
@@ -181,8 +184,11 @@ private:
     uint64_t done_batches_ = 0;
     // automatic GC (submitter thread only)
     int64_t gc_last_check_ = 0;       // steady ns
-    uint64_t gc_launched_ = 0;        // requests launched since the last count
-    uint64_t gc_budget_ = 0;          // requests that cannot fill any table past gc_high_pct
+    // requests launched since the last count that may insert into the
+    // token-bucket table [0] / the window and spill tables [1], and how many
+    // cannot fill them past gc_high_pct
+    uint64_t gc_launched_[2] = {0, 0};
+    uint64_t gc_budget_[2] = {0, 0};
     bool gc_counted_ = false;         // a first count was taken
     std::thread t_sub_, t_done_;
 };

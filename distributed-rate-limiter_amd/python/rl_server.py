@@ -317,6 +317,11 @@ def serve_native(co, limiters, address, io_threads=4, isolate=False, grace_s=5.0
                 signal.signal(sig, lambda *_: stop.set())
         stop.wait()
         srv.shutdown(grace_s)
+        if os.environ.get("RL_SERVER_STATS"):
+            import json
+            cs, gs = co.stats(), srv.stats()
+            print(json.dumps({"coalescer": {k: getattr(cs, k) for k, _ in cs._fields_[2:]},
+                              "grpc": {k: getattr(gs, k) for k, _ in gs._fields_[2:]}}), file=sys.stderr, flush=True)
     finally:
         srv.close()
     return srv.port

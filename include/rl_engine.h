@@ -111,6 +111,11 @@ int rl_engine_destroy(rl_engine* e);
  * its own id, as FormatKey(key) is unique per prefix (config.go:81-87). */
 int rl_config_register(rl_engine* e, uint8_t alg, int64_t limit, int64_t window_ns,
                        uint32_t* cfg_id);
+/* The state table a config's keys live in: 0 the token-bucket table, 1 the
+ * window table (whose keys may also move window keys to the spill table);
+ * RL_EINVAL for an unknown id.  The coalescer's automatic GC budgets each
+ * table by the requests that can insert into it. */
+int rl_config_table(rl_engine* e, uint32_t cfg_id);
 
 /* One batch in arrival order (array index = seq).  Host arrays; synchronous.
  *   ts_ns      request time, Unix ns (stands for time.Now() in AllowN)

@@ -529,3 +529,41 @@ def test_gpu_coalescer_gc_many_more_keys_than_slots(rl, oracle_mod):
     assert distinct > 4 * 4096 * 2
     assert st.gc_runs >= 3 and st.gc_failures == 0, (st.gc_runs, st.gc_failures)
     check_against_oracle(oracle_mod, cfgs, recs)
+
+
+@pytest.mark.gpu
+def test_gpu_coalescer_gc_budgets_each_table(rl, oracle_mod):
+    """the automatic GC budgets each table by the requests that can insert
+    into it (rl_config_table): token-bucket traffic in batches far larger than
+    a tiny window table's headroom triggers no GC and few counts (round 3: a
+    1024-slot window table made every batch of a token-bucket server count,
+    then collect, the tables)"""
+    cfgs = [(1, 20, 12 * NS), (3, 100, 60 * NS)]
+    eng = rl.Engine(profile=rl.PROFILE_REDIS7, tb_capacity=1 << 16, win_capacity=1024, max_batch=1 << 13,
+                    device=0, flags=rl.OPT_PIPELINE)
+    for a, L, W in cfgs:
+        eng.register(a, L, W)
+    co = rl.Coalescer(eng, max_batch=1 << 13, max_in_flight=3, gc_interval_ns=10 ** 12, gc_high_pct=50)
+    rng = np.random.default_rng(21)
+    recs = []
+    t = T0
+    for step in range(40):
+        m = 4000
+        key = rng.integers(0, 20_000, m).astype(np.uint64)
+        ts = (t + np.sort(rng.integers(0, 1_000_000, m))).astype(np.int64)
+        t += 1_000_000
+        n = np.ones(m, np.int64)
+        cfg = np.zeros(m, np.uint32)
+        if step % 10 == 9:                 # a few window requests now and then
+            cfg[:50] = 1
+        tk = co.submit(key, ts, n, cfg)
+        rc, res = co.wait(tk, m)
+        assert rc == 0, (step, rc)
+        recs.append((tk, key, ts, n, cfg, res))
+    st = co.stats()
+    co.close()
+    assert eng.sync() == 0
+    eng.close()
+    assert st.gc_runs == 0, st.gc_runs
+    assert st.gc_checks <= 8, st.gc_checks
+    check_against_oracle(oracle_mod, cfgs, recs)
