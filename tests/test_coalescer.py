@@ -565,5 +565,5 @@ def test_gpu_coalescer_gc_budgets_each_table(rl, oracle_mod):
     assert eng.sync() == 0
     eng.close()
     assert st.gc_runs == 0, st.gc_runs
-    assert st.gc_checks <= 8, st.gc_checks
+    assert st.gc_checks <= 20, st.gc_checks     # (every batch before: 40)
     check_against_oracle(oracle_mod, cfgs, recs)
