@@ -555,7 +555,8 @@ def main():
     os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=56,
+                    help="timed steps (default: batches 5-60 of the 64-batch configs[1] trace)")
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOAD_DESC),
