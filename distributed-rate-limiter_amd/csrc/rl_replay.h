@@ -558,13 +558,17 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
     __syncthreads();
     const uint32_t start = s_w[0][0] + s_w[1][0] + s_w[2][0] + s_w[3][0];
     const uint64_t lt = (1ull << lane) - 1ull;
-    const uint32_t base = (uint32_t)wave * (64 * LOC_ITEMS);
+    // every wave takes `per` consecutive rows of 64 elements (the fewest that
+    // cover the bucket), so all waves share the ranking work; wave order is
+    // element order (the passes stay stable)
+    const uint32_t per = (cnt + LOC_BLOCK - 1) / LOC_BLOCK;
+    const uint32_t base = (uint32_t)wave * (64 * per);
     // element e = base + 64 j + lane of the bucket, straight from HBM
     uint32_t key[LOC_ITEMS], val[LOC_ITEMS], rank[LOC_ITEMS];
 #pragma unroll
     for (int j = 0; j < LOC_ITEMS; j++) {
         const uint32_t e = base + j * 64 + lane;
-        const bool ok = e < cnt;
+        const bool ok = (uint32_t)j < per && e < cnt;
         key[j] = ok ? kin[start + e] : 0u;
         val[j] = ok ? vin[start + e] : 0u;
     }
@@ -574,20 +578,22 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < LOC_ITEMS; j++) {
-            const uint32_t e = base + j * 64 + lane;
-            const bool ok = e < cnt;
-            const uint32_t d = (key[j] >> shift) & ((1u << bits) - 1u);
-            uint64_t peers = __ballot(ok);
-            for (int bt = 0; bt < bits; bt++) {
-                const uint32_t bit = (d >> bt) & 1u;
-                const uint64_t bb = __ballot(bit);
-                peers &= bit ? bb : ~bb;
-            }
-            if (ok) {
-                const uint32_t below = __popcll(peers & lt);
-                const uint32_t cur = s_cnt[wave][d];
-                rank[j] = cur + below;
-                if (below == 0) s_cnt[wave][d] = cur + (uint32_t)__popcll(peers);
+            if ((uint32_t)j < per) {   // block-uniform
+                const uint32_t e = base + j * 64 + lane;
+                const bool ok = e < cnt;
+                const uint32_t d = (key[j] >> shift) & ((1u << bits) - 1u);
+                uint64_t peers = __ballot(ok);
+                for (int bt = 0; bt < bits; bt++) {
+                    const uint32_t bit = (d >> bt) & 1u;
+                    const uint64_t bb = __ballot(bit);
+                    peers &= bit ? bb : ~bb;
+                }
+                if (ok) {
+                    const uint32_t below = __popcll(peers & lt);
+                    const uint32_t cur = s_cnt[wave][d];
+                    rank[j] = cur + below;
+                    if (below == 0) s_cnt[wave][d] = cur + (uint32_t)__popcll(peers);
+                }
             }
         }
         __syncthreads();
@@ -616,7 +622,7 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
 #pragma unroll
         for (int j = 0; j < LOC_ITEMS; j++) {
             const uint32_t e = base + j * 64 + lane;
-            if (e < cnt) {
+            if ((uint32_t)j < per && e < cnt) {
                 const uint32_t d = (key[j] >> shift) & ((1u << bits) - 1u);
                 const uint32_t pos = s_base[d] + s_cnt[wave][d] + rank[j];
                 s_k[pos] = key[j];
@@ -627,22 +633,23 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
 #pragma unroll
         for (int j = 0; j < LOC_ITEMS; j++) {   // the next pass's elements, in the new order
             const uint32_t e = base + j * 64 + lane;
-            key[j] = e < cnt ? s_k[e] : 0u;
-            val[j] = e < cnt ? s_v[e] : 0u;
+            const bool ok = (uint32_t)j < per && e < cnt;
+            key[j] = ok ? s_k[e] : 0u;
+            val[j] = ok ? s_v[e] : 0u;
         }
     }
     if (low_bits <= 0) {   // (never: the MSD digit is the top 8 of >= 12 bits) keep s_k valid
 #pragma unroll
         for (int j = 0; j < LOC_ITEMS; j++) {
             const uint32_t e = base + j * 64 + lane;
-            if (e < cnt) s_k[e] = key[j];
+            if ((uint32_t)j < per && e < cnt) s_k[e] = key[j];
         }
         __syncthreads();
     }
 #pragma unroll
     for (int j = 0; j < LOC_ITEMS; j++) {
         const uint32_t e = base + j * 64 + lane;
-        if (e < cnt) {
+        if ((uint32_t)j < per && e < cnt) {
             kout[start + e] = key[j];
             vout[start + e] = val[j];
         }
@@ -656,7 +663,7 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
 #pragma unroll
     for (int j = 0; j < LOC_ITEMS; j++) {
         const uint32_t e = base + j * 64 + lane;
-        const bool ok = e < cnt;
+        const bool ok = (uint32_t)j < per && e < cnt;
         const bool valid = ok && key[j] != invalid_key;
         const bool head = valid && (e == 0 || s_k[e - 1] != key[j]);
         const bool bd = head || (ok && !valid);

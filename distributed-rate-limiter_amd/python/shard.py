@@ -112,6 +112,10 @@ class RoutedPipeline:
 
         self.R = new_stream()
         self.C = new_stream() if pg_cnt is not None else self.R
+        # one rank owns every key: nothing to exchange.  The records, counts and
+        # results stay where the pack / results kernels wrote them (the merge
+        # and unpack read them in place) -- no collective, no copy
+        self.local = world == 1 and not staged
         self.slots = []
         for _ in range(depth):
             s = dict(
@@ -121,7 +125,7 @@ class RoutedPipeline:
                 scnt=torch.zeros((world, INFO), dtype=torch.int64, device=d),   # per owner
                 rcnt=torch.zeros((world, INFO), dtype=torch.int64, device=d),   # per source
                 cnt_h=torch.zeros((2, world, INFO), dtype=torch.int64, pin_memory=self.cuda),
-                recv=torch.empty((mr, 4), dtype=torch.int64, device=d),
+                recv=None if self.local else torch.empty((mr, 4), dtype=torch.int64, device=d),
                 key=torch.empty(mr, dtype=torch.int64, device=d),
                 ts=torch.empty(mr, dtype=torch.int64, device=d),
                 n=torch.empty(mr, dtype=torch.int64, device=d),
@@ -133,7 +137,7 @@ class RoutedPipeline:
                 retry=torch.empty(mr, dtype=torch.int64, device=d),
                 reset=torch.empty(mr, dtype=torch.int64, device=d),
                 res=torch.empty((mr, 4), dtype=torch.int64, device=d),
-                back=torch.empty((mb, 4), dtype=torch.int64, device=d),
+                back=None if self.local else torch.empty((mb, 4), dtype=torch.int64, device=d),
                 S=new_stream(),
                 ev_cnt=None, ev_merged=None, ev_done=None, m=0, busy=False,
             )
@@ -190,10 +194,11 @@ class RoutedPipeline:
             self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]),
                           self._sp(C))
             self._tick("a_pack")
-            self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_cnt if self.pg_cnt is not None else self.pg_req)
+            if not self.local:
+                self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_cnt if self.pg_cnt is not None else self.pg_req)
             self._tick("a_a2a_cnt")
             s["cnt_h"][0].copy_(s["scnt"], non_blocking=True)
-            s["cnt_h"][1].copy_(s["rcnt"], non_blocking=True)
+            s["cnt_h"][1].copy_(s["rcnt" if not self.local else "scnt"], non_blocking=True)
             if self.cuda:
                 s["ev_cnt"] = torch.cuda.Event()
                 s["ev_cnt"].record(C)
@@ -215,15 +220,19 @@ class RoutedPipeline:
         assert tot <= self.max_recv, "received more than max_recv"
         self.last_recv = tot
         p = self._p
+        recv = s["send"] if self.local else s["recv"]
+        rcnt = s["scnt"] if self.local else s["rcnt"]
+
         def merge(stream):
             # the received info rows on the host too (read above): the merge is planned there
-            self.ops.merge(tot, p(s["recv"]), p(s["rcnt"]), p(s["cnt_h"][1]), p(s["key"]), p(s["ts"]), p(s["n"]),
+            self.ops.merge(tot, p(recv), p(rcnt), p(s["cnt_h"][1]), p(s["key"]), p(s["ts"]), p(s["n"]),
                            p(s["cfg"]), p(s["sms"]), p(s["at"]), self._sp(stream))
 
         with _ctx(self.R):
             if self.C is not self.R:
                 self.R.wait_event(s["ev_cnt"])    # the pack (send, rcnt) is complete
-            self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
+            if not self.local:
+                self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
             self._tick("b_a2a_req")
             if not self.merge_on_s:
                 merge(self.R)
@@ -247,9 +256,10 @@ class RoutedPipeline:
             self.ops.results(tot, p(s["at"]), p(s["dec"]), p(s["rem"]), p(s["retry"]), p(s["reset"]), p(s["res"]),
                              self._sp(S))
             self._tick("b_results")
-            self._a2a(s["back"][:m], s["res"][:tot], sc, rc, self.pg_res)
+            if not self.local:
+                self._a2a(s["back"][:m], s["res"][:tot], sc, rc, self.pg_res)
             self._tick("b_a2a_res")
-            self.ops.unpack(m, p(s["slot"]), p(s["back"]), p(dec), p(rem), p(retry), p(reset), self._sp(S))
+            self.ops.unpack(m, p(s["slot"]), p(s["res"] if self.local else s["back"]), p(dec), p(rem), p(retry), p(reset), self._sp(S))
             if S is not None:
                 s["ev_done"] = torch.cuda.Event()
                 s["ev_done"].record(S)
