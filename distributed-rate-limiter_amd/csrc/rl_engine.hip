@@ -506,6 +506,10 @@ struct rl_engine {
     uint32_t* d_eflags = nullptr;
     unsigned long long* d_count = nullptr;   // table counts / GC counters (rl_table_info_get, rl_table_gc)
     unsigned long long* h_count = nullptr;   // pinned host copy
+    // the grouping sort's last plan (1: every MSD bucket fit LDS), written by
+    // the MSD pass into mapped host memory; read when a batch is enqueued
+    uint32_t* h_plan = nullptr;
+    uint32_t* d_plan = nullptr;   // its device address
     uint32_t* stamp_ring = nullptr;   // RL_STAMP_KERNELS diagnostics
 
     // host-API staging (device side)
@@ -621,6 +625,7 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_eflags);
     (void)hipFree(e->d_count);
     if (e->h_count) (void)hipHostFree(e->h_count);
+    if (e->h_plan) (void)hipHostFree(e->h_plan);
     (void)hipFree(e->stamp_ring);
     (void)hipFree(e->small_kid);
     (void)hipFree(e->d_key); (void)hipFree(e->d_ts); (void)hipFree(e->d_n); (void)hipFree(e->d_sms); (void)hipFree(e->d_cfgid);
@@ -718,6 +723,11 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
     ok &= hipMalloc(&e->d_count, 8 * sizeof(unsigned long long)) == hipSuccess;
     ok &= hipHostMalloc(&e->h_count, 8 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess;
+    ok &= hipHostMalloc(&e->h_plan, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+    if (ok) {
+        *(volatile uint32_t*)e->h_plan = 0u;   // first batches: no prediction (the LSD passes are launched)
+        ok &= hipHostGetDevicePointer((void**)&e->d_plan, e->h_plan, 0) == hipSuccess;
+    }
     ok &= hipMalloc(&e->d_key, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_ts, 8 * M) == hipSuccess;
     ok &= hipMalloc(&e->d_n, 8 * M) == hipSuccess;
@@ -927,6 +937,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
     const int P = e->sort_passes;
+    bool pred_local = false;
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
@@ -942,30 +953,43 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         uint32_t* plan = B.ctrl + CTRL_PLAN;
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(B.sk0, B.sv0, B.sk1, B.sv1, m, e->sort_bits - 8, ghist,
                                                        B.status, B.ctrl + CTRL_TILE, e->d_eflags, nullptr, plan,
-                                                       LOC_MAX);
+                                                       LOC_MAX, e->d_plan);
         const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
         uint32_t* fk = odd ? B.sk0 : B.sk1;
         uint32_t* fv = odd ? B.sv0 : B.sv1;
-        k_sort_local<<<RADIX, LOC_BLOCK, 0, f>>>(B.sk1, B.sv1, fk, fv, ghist, e->sort_bits - 8, plan + 1,
-                                                 e->invalid_key, e->win_base, e->heavy_min, huge_min, lists);
+        // predicted plan: when the batch cannot hold a bucket too large for
+        // LDS, or the last plan the host sees had none, only k_sort_local is
+        // launched (it sorts a bucket too large for LDS itself, slowly: a
+        // misprediction costs time, never a result) -- no LSD passes and no
+        // k_segments, which would only find the plan flag and return
+        pred_local = m <= LOC_MAX || *(volatile uint32_t*)e->h_plan == 1u;
+        k_sort_local<<<RADIX, LOC_BLOCK, 0, f>>>(B.sk1, B.sv1, fk, fv, ghist, e->sort_bits - 8,
+                                                 pred_local ? nullptr : plan + 1, e->invalid_key, e->win_base,
+                                                 e->heavy_min, huge_min, lists, B.sk0, B.sv0);
+        if (pred_local) e->stats.sort_predicted++;
         kin = B.sk1;
         vin = B.sv1;
         kout = B.sk0;
         vout = B.sv0;
-        for (int p = 1; p < P; p++) {
+        for (int p = 1; p < P && !pred_local; p++) {
             uint32_t* status = B.status + (size_t)p * e->max_tiles * RADIX;
             k_sort_pass<false><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * (p - 1), ghist + p * RADIX,
                                                             status, B.ctrl + CTRL_TILE + p, e->d_eflags, plan);
             std::swap(kin, kout);
             std::swap(vin, vout);
         }
+        if (pred_local) {
+            kin = fk;
+            vin = fv;
+        }
         // kin / vin == fk / fv
     }
     if (tall) (void)hipEventRecord(ev[2], f);
     // sorted keys/values are now in kin/vin
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
-    k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min, huge_min, lists,
-                                             P > 1 ? B.ctrl + CTRL_PLAN : nullptr);
+    if (!pred_local)
+        k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min, huge_min, lists,
+                                                 P > 1 ? B.ctrl + CTRL_PLAN : nullptr);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     // (the server clock only when the caller gave one: else floor(ts / 1e6) where it is read)
     ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, nullptr, nullptr, nullptr,

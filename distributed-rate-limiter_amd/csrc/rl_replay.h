@@ -536,17 +536,254 @@ constexpr int LOC_ITEMS = 12;
 constexpr uint32_t LOC_MAX = LOC_BLOCK * LOC_ITEMS;   // 12288 elements per bucket
 constexpr int LOC_WAVES = LOC_BLOCK / 64;
 
+// A bucket larger than LDS, met only when the engine launched the grouping
+// sort for "every bucket fits" on a prediction (the previous batches' plans,
+// rl_engine.hip) that this batch breaks: the block sorts its bucket alone,
+// with stable LSD passes over the bucket's range in HBM -- LOC_MAX elements
+// at a time ranked in LDS as in k_sort_local, scattered at running digit
+// offsets -- ping-ponging between (kin, vin) and the free MSD input buffers
+// (xk, xv) so the last pass lands in (kout, vout), which is one of the two;
+// then it builds the bucket's segment lists chunk by chunk (a segment running
+// past a chunk ends where wave_seg_end finds it).  Slow (one CU), correct,
+// and rare: a misprediction costs one batch this path, after which the engine
+// launches the LSD passes again.
+__device__ __noinline__ void loc_sort_big(const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                                          uint32_t* xk, uint32_t* xv, uint32_t start, uint32_t cnt, int low_bits,
+                                          uint32_t invalid_key, uint32_t win_base, uint32_t heavy_min,
+                                          uint32_t huge_min, SegLists L, uint32_t* s_k, uint32_t* s_v,
+                                          uint32_t (*s_cnt)[RADIX], uint32_t* s_base, uint32_t (*s_w)[4],
+                                          uint32_t* s_lbase, uint32_t* s_run) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const int npass = (low_bits + 7) / 8;
+    // buffers: P0 = (kin, vin), P1 = (xk, xv); the passes alternate from P0
+    // and end in P(npass mod 2), which must be kout's: else copy P0 to P1 first
+    const uint32_t *sk = kin, *sv = vin;
+    uint32_t *dk = xk, *dv = xv;
+    const bool out_p0 = kout == kin;
+    if (out_p0 != ((npass & 1) == 0)) {
+        for (uint32_t e = tid; e < cnt; e += LOC_BLOCK) {
+            xk[start + e] = kin[start + e];
+            xv[start + e] = vin[start + e];
+        }
+        __threadfence();
+        __syncthreads();
+        sk = xk;
+        sv = xv;
+        dk = const_cast<uint32_t*>(kin);
+        dv = const_cast<uint32_t*>(vin);
+    }
+    for (int pass = 0; pass < npass; pass++) {
+        const int shift = 8 * pass;
+        const int bits = low_bits - shift < 8 ? low_bits - shift : 8;
+        const uint32_t dm = (1u << bits) - 1u;
+        if (tid < RADIX) s_run[tid] = 0;
+        __syncthreads();
+        for (uint32_t e = tid; e < cnt; e += LOC_BLOCK) atomicAdd(&s_run[(sk[start + e] >> shift) & dm], 1u);
+        __syncthreads();
+        {   // exclusive scan of the digit counts (threads < RADIX: 4 waves)
+            const uint32_t v = tid < RADIX ? s_run[tid] : 0u;
+            uint32_t inc = v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = __shfl_up(inc, off, 64);
+                if (lane >= off) inc += t;
+            }
+            if (tid < RADIX && lane == 63) s_w[wave][0] = inc;
+            __syncthreads();
+            if (tid < RADIX) {
+                uint32_t wp = 0;
+                for (int w = 0; w < wave; w++) wp += s_w[w][0];
+                s_run[tid] = wp + inc - v;
+            }
+            __syncthreads();
+        }
+        for (uint32_t c0 = 0; c0 < cnt; c0 += LOC_MAX) {
+            const uint32_t ccnt = min((uint32_t)LOC_MAX, cnt - c0);
+            const uint32_t per = (ccnt + LOC_BLOCK - 1) / LOC_BLOCK;
+            const uint32_t base = (uint32_t)wave * (64 * per);
+            uint32_t key[LOC_ITEMS], val[LOC_ITEMS], rank[LOC_ITEMS];
+            for (int d = tid; d < LOC_WAVES * RADIX; d += LOC_BLOCK) (&s_cnt[0][0])[d] = 0;
+#pragma unroll
+            for (int j = 0; j < LOC_ITEMS; j++) {
+                const uint32_t e = base + j * 64 + lane;
+                const bool ok = (uint32_t)j < per && e < ccnt;
+                key[j] = ok ? sk[start + c0 + e] : 0u;
+                val[j] = ok ? sv[start + c0 + e] : 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < LOC_ITEMS; j++) {
+                if ((uint32_t)j < per) {   // block-uniform
+                    const uint32_t e = base + j * 64 + lane;
+                    const bool ok = e < ccnt;
+                    const uint32_t d = (key[j] >> shift) & dm;
+                    uint64_t peers = __ballot(ok);
+                    for (int bt = 0; bt < bits; bt++) {
+                        const uint32_t bit = (d >> bt) & 1u;
+                        const uint64_t bb = __ballot(bit);
+                        peers &= bit ? bb : ~bb;
+                    }
+                    if (ok) {
+                        const uint32_t below = __popcll(peers & lt);
+                        const uint32_t cur = s_cnt[wave][d];
+                        rank[j] = cur + below;
+                        if (below == 0) s_cnt[wave][d] = cur + (uint32_t)__popcll(peers);
+                    }
+                }
+            }
+            __syncthreads();
+            if (tid < RADIX) {   // per digit: exclusive prefix over the waves, chunk total
+                uint32_t tot = 0;
+                for (int w = 0; w < LOC_WAVES; w++) {
+                    const uint32_t c = s_cnt[w][tid];
+                    s_cnt[w][tid] = tot;
+                    tot += c;
+                }
+                s_base[tid] = tot;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < LOC_ITEMS; j++) {
+                const uint32_t e = base + j * 64 + lane;
+                if ((uint32_t)j < per && e < ccnt) {
+                    const uint32_t d = (key[j] >> shift) & dm;
+                    const uint32_t pos = s_run[d] + s_cnt[wave][d] + rank[j];
+                    dk[start + pos] = key[j];
+                    dv[start + pos] = val[j];
+                }
+            }
+            __syncthreads();
+            if (tid < RADIX) s_run[tid] += s_base[tid];
+            __syncthreads();
+        }
+        __threadfence();   // this pass's stores before the next pass's loads (other waves, L1)
+        __syncthreads();
+        const uint32_t* tk = sk;
+        const uint32_t* tv = sv;
+        sk = dk;
+        sv = dv;
+        dk = const_cast<uint32_t*>(tk);
+        dv = const_cast<uint32_t*>(tv);
+    }
+    // segment lists of the sorted bucket (kout), chunk by chunk
+    const uint32_t* kb = kout + start;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += LOC_MAX) {
+        const uint32_t ccnt = min((uint32_t)LOC_MAX, cnt - c0);
+        const uint32_t per = (ccnt + LOC_BLOCK - 1) / LOC_BLOCK;
+        const uint32_t base = (uint32_t)wave * (64 * per);
+        uint32_t key[LOC_ITEMS], bnd[LOC_ITEMS], head[LOC_ITEMS];
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            const uint32_t e = base + j * 64 + lane;
+            key[j] = ((uint32_t)j < per && e < ccnt) ? kb[c0 + e] : 0u;
+            if ((uint32_t)j < per && e < ccnt) s_k[e] = key[j];
+        }
+        const uint32_t kprev = kb[c0 ? c0 - 1 : 0];
+        if (tid == 0) s_lbase[0] = SEG_NONE;   // the chunk's open head (its end lies past the chunk)
+        __syncthreads();
+        uint32_t run = 0;
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            const uint32_t e = base + j * 64 + lane;
+            const bool ok = (uint32_t)j < per && e < ccnt;
+            const bool valid = ok && key[j] != invalid_key;
+            const uint32_t before = e ? s_k[e ? e - 1 : 0] : kprev;
+            const bool hd = valid && ((c0 == 0 && e == 0) || before != key[j]);
+            const bool bd = hd || (ok && !valid);
+            const uint64_t bm = __ballot(bd);
+            bnd[j] = bd ? run + (uint32_t)__popcll(bm & lt) : SEG_NONE;
+            head[j] = hd ? 1u : 0u;
+            run += (uint32_t)__popcll(bm);
+        }
+        if (lane == 0) s_w[wave][0] = run;
+        __syncthreads();
+        uint32_t wpre = 0, nb = 0;
+        for (int w = 0; w < LOC_WAVES; w++) {
+            const uint32_t c = s_w[w][0];
+            wpre += w < wave ? c : 0u;
+            nb += c;
+        }
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            if (bnd[j] != SEG_NONE) {
+                bnd[j] += wpre;
+                s_v[bnd[j]] = base + j * 64 + lane;
+            }
+        }
+        __syncthreads();
+        // the last boundary of the chunk, if a head, ends past the chunk
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++)
+            if (head[j] && bnd[j] + 1 == nb && c0 + ccnt < cnt) s_lbase[0] = base + j * 64 + lane;
+        __syncthreads();
+        if (s_lbase[0] != SEG_NONE && wave == 0) {
+            const uint32_t o = s_lbase[0];
+            const uint32_t e = wave_seg_end(kb, cnt, c0 + ccnt, s_k[o]);
+            if (lane == 0) s_lbase[1] = e - c0;
+        }
+        __syncthreads();
+        const uint32_t open_end = s_lbase[1];
+        uint32_t which[LOC_ITEMS], len[LOC_ITEMS];
+        uint32_t lrun[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            which[j] = 4u;
+            len[j] = 0u;
+            if (head[j]) {
+                const uint32_t e = base + j * 64 + lane;
+                const uint32_t end = bnd[j] + 1 < nb ? s_v[bnd[j] + 1] : c0 + ccnt < cnt ? open_end : ccnt;
+                len[j] = end - e;
+                const bool tb = key[j] < win_base;
+                which[j] = len[j] < heavy_min ? 1u : !tb ? 2u : len[j] >= huge_min ? 3u : 0u;
+            }
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const uint64_t wm = __ballot(which[j] == (uint32_t)w);
+                if (which[j] == (uint32_t)w) bnd[j] = lrun[w] + (uint32_t)__popcll(wm & lt);
+                lrun[w] += (uint32_t)__popcll(wm);
+            }
+        }
+        __syncthreads();   // s_w reused
+        if (lane == 0)
+            for (int w = 0; w < 4; w++) s_w[wave][w] = lrun[w];
+        __syncthreads();
+        if (tid < 4) {
+            uint32_t t = 0;
+            for (int w = 0; w < LOC_WAVES; w++) t += s_w[w][tid];
+            s_base[tid] = t ? atomicAdd(&L.count[tid], t) : 0u;
+        }
+        __syncthreads();
+        uint32_t wb[4];
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+            uint32_t x = s_base[w];
+            for (int v = 0; v < wave; v++) x += s_w[v][w];
+            wb[w] = x;
+        }
+#pragma unroll
+        for (int j = 0; j < LOC_ITEMS; j++) {
+            if (which[j] < 4u) {
+                const uint32_t w = which[j];
+                const uint32_t at = (w == 0 ? wb[0] : w == 1 ? wb[1] : w == 2 ? wb[2] : wb[3]) + bnd[j];
+                L.list[w][at] = SegRec{start + c0 + base + j * 64 + lane, len[j]};
+            }
+        }
+        __syncthreads();   // s_k, s_v, s_w, s_base, s_lbase reused by the next chunk
+    }
+}
+
 __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
                                                           uint32_t* vout, const uint32_t* __restrict__ ghist_msd,
                                                           int low_bits, const uint32_t* skip, uint32_t invalid_key,
                                                           uint32_t win_base, uint32_t heavy_min, uint32_t huge_min,
-                                                          SegLists L) {
-    if (*skip) return;
+                                                          SegLists L, uint32_t* xk, uint32_t* xv) {
+    if (skip && *skip) return;
     __shared__ uint32_t s_k[LOC_MAX], s_v[LOC_MAX];
     __shared__ uint32_t s_cnt[LOC_WAVES][RADIX];
     __shared__ uint32_t s_base[RADIX];
     __shared__ uint32_t s_w[LOC_WAVES][4];
     __shared__ uint32_t s_lbase[4];
+    __shared__ uint32_t s_run[RADIX];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t cnt = ghist_msd[b];
@@ -557,6 +794,12 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
     if (lane == 0 && wave < 4) s_w[wave][0] = pre;
     __syncthreads();
     const uint32_t start = s_w[0][0] + s_w[1][0] + s_w[2][0] + s_w[3][0];
+    if (cnt > LOC_MAX) {   // only in a launch without `skip` (a predicted plan; see loc_sort_big)
+        __syncthreads();   // s_w
+        loc_sort_big(kin, vin, kout, vout, xk, xv, start, cnt, low_bits, invalid_key, win_base, heavy_min, huge_min,
+                     L, s_k, s_v, s_cnt, s_base, s_w, s_lbase, s_run);
+        return;
+    }
     const uint64_t lt = (1ull << lane) - 1ull;
     // every wave takes `per` consecutive rows of 64 elements (the fewest that
     // cover the bucket), so all waves share the ranking work; wave order is

@@ -69,13 +69,14 @@ __device__ inline uint32_t block_excl_scan_256(uint32_t v, uint32_t* s_tmp /*[4]
 // skip (nullable): a device flag that turns the pass into a no-op.
 // plan (nullable, the MSD pass of the grouping sort): the block of tile 0
 // writes plan[0] = 1 when no digit of this pass holds more than plan_cap
-// elements (every bucket then fits k_sort_local) and plan[1] = 1 otherwise.
+// elements (every bucket then fits k_sort_local) and plan[1] = 1 otherwise,
+// and plan[0] to plan_host (nullable) too.
 template <bool FIRST>
 __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, uint32_t m, int shift, const uint32_t* __restrict__ ghist,
     uint32_t* status, uint32_t* tile_ctr, uint32_t* eflags, const uint32_t* skip = nullptr,
-    uint32_t* plan = nullptr, uint32_t plan_cap = 0) {
+    uint32_t* plan = nullptr, uint32_t plan_cap = 0, uint32_t* plan_host = nullptr) {
     if (skip && *skip) return;
     __shared__ uint32_t s_wcnt[SORT_WAVES][RADIX];
     __shared__ uint32_t s_goff[RADIX];
@@ -164,6 +165,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
             for (int w = 1; w < SORT_WAVES; w++) mx = max(mx, s_tmp[w]);
             plan[0] = mx <= plan_cap ? 1u : 0u;
             plan[1] = mx <= plan_cap ? 0u : 1u;
+            if (plan_host) plan_host[0] = plan[0];   // mapped host word: the engine's next prediction
         }
         __syncthreads();
     }

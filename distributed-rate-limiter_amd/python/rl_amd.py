@@ -70,6 +70,7 @@ class rl_stats(_Sized):
         ("sort_passes", C.c_uint32),
         ("stamp_cycles", C.c_uint64 * 7),
         ("coop_ends", C.c_uint64 * 4),
+        ("sort_predicted", C.c_uint64),
     ]
 
 

@@ -228,21 +228,32 @@ class RoutedPipeline:
             self.ops.merge(tot, p(recv), p(rcnt), p(s["cnt_h"][1]), p(s["key"]), p(s["ts"]), p(s["n"]),
                            p(s["cfg"]), p(s["sms"]), p(s["at"]), self._sp(stream))
 
-        with _ctx(self.R):
-            if self.C is not self.R:
-                self.R.wait_event(s["ev_cnt"])    # the pack (send, rcnt) is complete
-            if not self.local:
-                self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
-            self._tick("b_a2a_req")
+        if self.local:
+            # nothing to exchange: the merge waits for this step's pack only
+            # (an event on R would also order it after the later steps'
+            # packs issued since)
+            s["ev_merged"] = s["ev_cnt"]
             if not self.merge_on_s:
-                merge(self.R)
-            if self.cuda:
-                s["ev_merged"] = torch.cuda.Event()
-                s["ev_merged"].record(self.R)
-            self._tick("b_merge")
+                with _ctx(self.R):
+                    merge(self.R)
+                    if self.cuda:
+                        s["ev_merged"] = torch.cuda.Event()
+                        s["ev_merged"].record(self.R)
+        else:
+            with _ctx(self.R):
+                if self.C is not self.R:
+                    self.R.wait_event(s["ev_cnt"])    # the pack (send, rcnt) is complete
+                self._a2a(s["recv"][:tot], s["send"][:m], rc, sc, self.pg_req)
+                self._tick("b_a2a_req")
+                if not self.merge_on_s:
+                    merge(self.R)
+                if self.cuda:
+                    s["ev_merged"] = torch.cuda.Event()
+                    s["ev_merged"].record(self.R)
+        self._tick("b_merge")
         S = s["S"]
         with _ctx(S):
-            if S is not None:
+            if S is not None and s["ev_merged"] is not None:
                 S.wait_event(s["ev_merged"])
             if self.merge_on_s:
                 if self.ev_last_merge is not None:

@@ -99,6 +99,8 @@ typedef struct rl_stats {
     uint64_t coop_ends[4];     /* how the last batch's cooperative rounds ended: [0] window done,
                                   [1] stop request (allow / clamp / decade / expiry), [2] boundary
                                   (exact-pass mismatch safety net), [3] offset iteration cap */
+    uint64_t sort_predicted;   /* batches whose grouping sort was launched as k_sort_local only (every
+                                  MSD bucket predicted to fit LDS: no LSD passes, no k_segments) */
 } rl_stats;
 
 /* replaces redis.NewClient + NewTokenBucket/NewSlidingWindow/NewFixedWindow's

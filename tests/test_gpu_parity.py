@@ -213,6 +213,42 @@ def test_sort_local_and_lsd_paths(rl, counts):
         run_both(rl, profile, configs, split((key, ts, n, cfg, None), [m]), tb=1 << 16, win=1 << 16)
 
 
+def test_sort_predicted_plan_and_misprediction(rl):
+    # once a batch's MSD buckets all fit LDS the engine launches the next
+    # batches' grouping sort as k_sort_local alone; a batch that then brings a
+    # bucket too large for LDS (hot keys, one spanning three LDS chunks) is
+    # sorted by k_sort_local's in-kernel LSD path (loc_sort_big) on that
+    # misprediction, and the batches after it go back to the LSD passes until
+    # a plan fits again -- every batch against the oracle
+    configs = CONFIG_SETS["mixed"]
+    rng = np.random.default_rng(5)
+    batches, t = [], T0
+    for kind in ["u", "u", "u", "hot", "hot", "u", "u"]:
+        m = 60_000
+        key = rng.integers(1000, 200_000, m).astype(np.uint64)
+        if kind == "hot":
+            r = rng.random(m)
+            key[r < 0.5] = 77                      # 30k requests of one key
+            key[(r >= 0.5) & (r < 0.75)] = 78      # and 15k of another algorithm's
+        ts = t + np.cumsum(rng.integers(0, 300_000, m)).astype(np.int64)
+        t = int(ts[-1])
+        n = rng.choice([1, 1, 2], m).astype(np.int64)
+        n[rng.random(m) < 0.003] = 0
+        batches.append((key, ts, n, (key % len(configs)).astype(np.uint32), None))
+    eng = make_engine(rl, 0, tb=1 << 18, win=1 << 18)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        assert eng.register(a, L, W) == sim.add_config(a, L, W)
+    pred = []
+    for i, (key, ts, n, cfg, sms) in enumerate(batches):
+        before = eng.stats().sort_predicted
+        res = eng.decide(key, ts, n, cfg, sms)
+        assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
+        pred.append(int(eng.stats().sort_predicted - before))
+    # (batch 0 follows the engine's warm-up batch, whose plan fit)
+    assert pred[1:] == [1, 1, 1, 0, 0, 1]       # batch 3 (hot) mispredicted: loc_sort_big
+
+
 def test_single_hot_key_full_batch(rl):
     # the bench's diagnostic workload: one key carries the whole 1M batch
     g = traces.TokenBucketZipf(nkeys=1, batch=1_000_000)
