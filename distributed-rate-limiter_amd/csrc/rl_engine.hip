@@ -923,21 +923,24 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // atomics per block on 768 shared words) stays cheap
     const int probe_grid = (int)std::min<uint32_t>((m + PROBE_BLOCK - 1) / PROBE_BLOCK, (uint32_t)e->probe_grid);
     const bool xs = a.sms != nullptr;   // explicit server clock: 32-byte request records
+    // the grouping sort's predicted plan (below): with k_sort_local alone only
+    // the MSD histogram is used, so the probe counts that pass only
+    const bool pred_local = e->sort_passes > 1 && (m <= LOC_MAX || *(volatile uint32_t*)e->h_plan == 1u);
+    const int hist_passes = pred_local ? 1 : e->sort_passes;
     if (xs)
         k_probe<1, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
-            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, e->sort_shifts, a,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
             static_cast<ReqRec<true>*>(B.rec), e->d_eflags);
     else
         k_probe<1, false><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
-            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, e->sort_passes, e->sort_shifts, a,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
             static_cast<ReqRec<false>*>(B.rec), e->d_eflags);
     if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
     const int P = e->sort_passes;
-    bool pred_local = false;
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
@@ -962,7 +965,6 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         // launched (it sorts a bucket too large for LDS itself, slowly: a
         // misprediction costs time, never a result) -- no LSD passes and no
         // k_segments, which would only find the plan flag and return
-        pred_local = m <= LOC_MAX || *(volatile uint32_t*)e->h_plan == 1u;
         k_sort_local<<<RADIX, LOC_BLOCK, 0, f>>>(B.sk1, B.sv1, fk, fv, ghist, e->sort_bits - 8,
                                                  pred_local ? nullptr : plan + 1, e->invalid_key, e->win_base,
                                                  e->heavy_min, huge_min, lists, B.sk0, B.sv0);
