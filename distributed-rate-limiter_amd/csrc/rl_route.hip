@@ -480,6 +480,120 @@ __global__ __launch_bounds__(RT_BLOCK) void k_merge_gather(uint32_t m, MergePlan
     }
 }
 
+// ---- the single-source merge planned on the device (world 1) ----------------
+// One source: the received order is the decision order, and a request arrives
+// at the running max of ts so far (= ts when the batch is in time order).  No
+// host reads anything: a per-tile max, one scan block that also advances the
+// store clock (a device word: the merges run in step order), one gather.
+constexpr unsigned long long TS_BIAS = 1ull << 63;   // int64 order as uint64 order
+
+__global__ __launch_bounds__(RT_BLOCK) void k_m1_tmax(uint32_t m, const rl_route_rec* __restrict__ rec,
+                                                      unsigned long long* tmax) {
+    __shared__ unsigned long long s_w[RT_BLOCK / 64];
+    unsigned long long mx = 0;
+#pragma unroll
+    for (int q = 0; q < MT_ITEMS; q++) {
+        const uint32_t i = blockIdx.x * MT_TILE + threadIdx.x * MT_ITEMS + q;
+        if (i < m) {
+            const unsigned long long c = (unsigned long long)rec[i].ts ^ TS_BIAS;
+            mx = c > mx ? c : mx;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(mx, off);
+        mx = o > mx ? o : mx;
+    }
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < RT_BLOCK / 64; w++) mx = s_w[w] > mx ? s_w[w] : mx;
+        tmax[blockIdx.x] = mx;
+    }
+}
+
+// exclusive running max over the tiles (in place); then tmax[tiles] = the
+// clock of the earlier steps (for the gather) and the clock advances to
+// max(clock, floor(latest ts / 1e6)) -- what the host plan does with the info rows
+__global__ __launch_bounds__(1024) void k_m1_tscan(uint32_t tiles, unsigned long long* tmax, int64_t* clock) {
+    __shared__ unsigned long long s_w[16];
+    __shared__ unsigned long long s_carry;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t t0 = 0; t0 < tiles; t0 += 1024) {
+        const uint32_t t = t0 + tid;
+        const unsigned long long v = t < tiles ? tmax[t] : 0ull;
+        unsigned long long inc = v;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long u = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc = u > inc ? u : inc;
+        }
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        unsigned long long pre = s_carry;
+        for (uint32_t k = 0; k < w; k++) pre = s_w[k] > pre ? s_w[k] : pre;
+        unsigned long long ex = __shfl_up(inc, 1, 64);
+        ex = lane ? (ex > pre ? ex : pre) : pre;
+        __syncthreads();
+        if (t < tiles) tmax[t] = ex;
+        if (tid == 1023) s_carry = inc > pre ? inc : pre;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        const int64_t c0 = *clock;
+        tmax[tiles] = (unsigned long long)c0;
+        const int64_t ms = floor_div((int64_t)(s_carry ^ TS_BIAS), 1000000LL);
+        *clock = ms > c0 ? ms : c0;
+    }
+}
+
+// the engine's inputs in received order, server clock from the running max
+__global__ __launch_bounds__(RT_BLOCK) void k_m1_gather(uint32_t m, uint32_t tiles, const rl_route_rec* __restrict__ rec,
+                                                        const unsigned long long* __restrict__ tpre,
+                                                        uint64_t* __restrict__ key, int64_t* __restrict__ ts,
+                                                        int64_t* __restrict__ n, uint32_t* __restrict__ cfg,
+                                                        int64_t* __restrict__ sms, uint32_t* __restrict__ at) {
+    __shared__ unsigned long long s_w[RT_BLOCK / 64];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t i0 = blockIdx.x * MT_TILE + threadIdx.x * MT_ITEMS;
+    const int64_t c0 = (int64_t)tpre[tiles];
+    rl_route_rec r[MT_ITEMS];
+    unsigned long long c[MT_ITEMS];
+    unsigned long long run = 0;
+#pragma unroll
+    for (int q = 0; q < MT_ITEMS; q++) {
+        const uint32_t i = i0 + q;
+        if (i < m) r[q] = rec[i];
+        c[q] = i < m ? (unsigned long long)r[q].ts ^ TS_BIAS : 0ull;
+        run = c[q] > run ? c[q] : run;
+        c[q] = run;                                  // inclusive within the thread
+    }
+    unsigned long long inc = run;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long u = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc = u > inc ? u : inc;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    unsigned long long pre = tpre[blockIdx.x];
+    for (uint32_t k = 0; k < w; k++) pre = s_w[k] > pre ? s_w[k] : pre;
+    unsigned long long ex = __shfl_up(inc, 1, 64);
+    ex = lane ? (ex > pre ? ex : pre) : pre;
+#pragma unroll
+    for (int q = 0; q < MT_ITEMS; q++) {
+        const uint32_t i = i0 + q;
+        if (i >= m) continue;
+        const unsigned long long a = c[q] > ex ? c[q] : ex;
+        const int64_t ms = floor_div((int64_t)(a ^ TS_BIAS), 1000000LL);
+        key[i] = r[q].key;
+        ts[i] = r[q].ts;
+        n[i] = r[q].n;
+        cfg[i] = r[q].cfg;
+        sms[i] = ms > c0 ? ms : c0;
+        at[i] = i;
+    }
+}
+
 __global__ __launch_bounds__(RT_BLOCK) void k_route_results(uint32_t m, const uint32_t* __restrict__ at,
                                                             const uint8_t* __restrict__ dec,
                                                             const int64_t* __restrict__ rem,
@@ -524,6 +638,8 @@ struct rl_router {
     uint32_t* d_status = nullptr;    // sticky router status: the sort's look-back flags
     uint32_t host_status = 0;        // sticky router status found by the host plan (RS_*)
     int64_t clock = INT64_MIN;        // the store clock of the next step (ms), kept in enqueue order
+    int64_t* d_clock = nullptr;       // the same, on the device, for merges planned there (world 1)
+    bool clock_on_device = false;     // a device-planned merge has run: the clock lives in d_clock
 };
 
 extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t max_recv,
@@ -546,7 +662,8 @@ extern "C" int rl_router_create(int32_t device, int32_t world, uint32_t max_batc
     ok = ok && hipMalloc(&r->ctrl, 4 * (MC_WORDS + (size_t)MERGE_PASSES * stiles * RADIX)) == hipSuccess;
     for (uint32_t** p : {&r->k0, &r->k1, &r->v0, &r->v1}) ok = ok && hipMalloc(p, 4 * (size_t)max_recv) == hipSuccess;
     ok = ok && hipMalloc(&r->kk, 8 * (size_t)max_recv) == hipSuccess;
-    ok = ok && hipMalloc(&r->tmax, 8 * ((size_t)max_recv / MT_TILE + 1)) == hipSuccess;
+    ok = ok && hipMalloc(&r->tmax, 8 * ((size_t)max_recv / MT_TILE + 2)) == hipSuccess;
+    ok = ok && hipMalloc(&r->d_clock, 8) == hipSuccess;
     ok = ok && hipMalloc(&r->d_status, 4) == hipSuccess && hipMemset(r->d_status, 0, 4) == hipSuccess;
     if (!ok) {
         rl_router_destroy(r);
@@ -561,7 +678,7 @@ extern "C" int rl_router_destroy(rl_router* r) {
     if (!r) return RL_EINVAL;
     (void)hipSetDevice(r->device);
     for (void* p : {(void*)r->tile_cnt, (void*)r->ctrl, (void*)r->k0, (void*)r->k1, (void*)r->v0, (void*)r->v1,
-                    (void*)r->kk, (void*)r->tmax,
+                    (void*)r->kk, (void*)r->tmax, (void*)r->d_clock,
                     (void*)r->d_status, (void*)r->tile_off, (void*)r->psum})
         (void)hipFree(p);
     delete r;
@@ -633,11 +750,27 @@ __global__ void k_merge_status(const uint32_t* sort_flags, uint32_t* status) {
 extern "C" int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info,
                               const int64_t* recv_info_host, uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg,
                               int64_t* server_ms, uint32_t* at, void* stream) {
-    if (!r || !recv_info || !recv_info_host || m_recv > r->max_recv ||
-        (m_recv && (!recv || !key || !ts || !n || !cfg || !server_ms || !at)))
+    if (!r || !recv_info || m_recv > r->max_recv || (m_recv && (!recv || !key || !ts || !n || !cfg || !server_ms || !at)))
         return RL_EINVAL;
     (void)hipSetDevice(r->device);
     hipStream_t s = (hipStream_t)stream;
+    if (!recv_info_host) {
+        // planned on the device: one source only (world 1), nothing read by the host
+        if (r->world != 1) return RL_EINVAL;
+        if (!r->clock_on_device) {
+            if (hipMemcpyAsync(r->d_clock, &r->clock, 8, hipMemcpyHostToDevice, s) != hipSuccess) return RL_EDEVICE;
+            if (hipStreamSynchronize(s) != hipSuccess) return RL_EDEVICE;
+            r->clock_on_device = true;
+        }
+        const uint32_t m = (uint32_t)m_recv;
+        if (!m) return RL_OK;
+        const uint32_t mtiles = (m + MT_TILE - 1) / MT_TILE;
+        k_m1_tmax<<<mtiles, RT_BLOCK, 0, s>>>(m, recv, r->tmax);
+        k_m1_tscan<<<1, 1024, 0, s>>>(mtiles, r->tmax, r->d_clock);
+        k_m1_gather<<<mtiles, RT_BLOCK, 0, s>>>(m, mtiles, recv, r->tmax, key, ts, n, cfg, server_ms, at);
+        return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+    }
+    if (r->clock_on_device) return RL_EINVAL;   // the clock is the device's now: keep planning there
     // the plan, on the host: the time-key origin and span of the sources that
     // sent records, whether a source is out of time order, the passes
     int64_t lo = INT64_MAX, hi = INT64_MIN, clock_next = r->clock;

@@ -195,10 +195,11 @@ class RoutedPipeline:
                           self._sp(C))
             self._tick("a_pack")
             if not self.local:
+                # the host reads the counts to size the record exchange
                 self._a2a(s["rcnt"], s["scnt"], None, None, self.pg_cnt if self.pg_cnt is not None else self.pg_req)
-            self._tick("a_a2a_cnt")
-            s["cnt_h"][0].copy_(s["scnt"], non_blocking=True)
-            s["cnt_h"][1].copy_(s["rcnt" if not self.local else "scnt"], non_blocking=True)
+                self._tick("a_a2a_cnt")
+                s["cnt_h"][0].copy_(s["scnt"], non_blocking=True)
+                s["cnt_h"][1].copy_(s["rcnt"], non_blocking=True)
             if self.cuda:
                 s["ev_cnt"] = torch.cuda.Event()
                 s["ev_cnt"].record(C)
@@ -208,15 +209,21 @@ class RoutedPipeline:
         results back into dec/rem/retry/reset (device tensors, batch order);
         returns the stream on which they are complete"""
         s = self.slots[b % self.depth]
-        if s["ev_cnt"] is not None:
-            t0 = time.perf_counter()
-            s["ev_cnt"].synchronize()
-            self.wait_s += time.perf_counter() - t0
-        self._tick("b_wait")
-        sc = s["cnt_h"][0][:, 0].tolist()
-        rc = s["cnt_h"][1][:, 0].tolist()
-        self._tick("b_counts")
-        tot, m = int(sum(rc)), s["m"]
+        if self.local:
+            # world 1: every record is this rank's and the merge is planned on
+            # the device (rl_route_merge without host rows): nothing to wait for
+            m = tot = s["m"]
+            sc = rc = [m]
+        else:
+            if s["ev_cnt"] is not None:
+                t0 = time.perf_counter()
+                s["ev_cnt"].synchronize()
+                self.wait_s += time.perf_counter() - t0
+            self._tick("b_wait")
+            sc = s["cnt_h"][0][:, 0].tolist()
+            rc = s["cnt_h"][1][:, 0].tolist()
+            self._tick("b_counts")
+            tot, m = int(sum(rc)), s["m"]
         assert tot <= self.max_recv, "received more than max_recv"
         self.last_recv = tot
         p = self._p
@@ -225,7 +232,8 @@ class RoutedPipeline:
 
         def merge(stream):
             # the received info rows on the host too (read above): the merge is planned there
-            self.ops.merge(tot, p(recv), p(rcnt), p(s["cnt_h"][1]), p(s["key"]), p(s["ts"]), p(s["n"]),
+            self.ops.merge(tot, p(recv), p(rcnt), None if self.local else p(s["cnt_h"][1]), p(s["key"]), p(s["ts"]),
+                           p(s["n"]),
                            p(s["cfg"]), p(s["sms"]), p(s["at"]), self._sp(stream))
 
         if self.local:

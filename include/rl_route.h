@@ -111,7 +111,10 @@ int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts
  * order, arrival = ts and no running max is taken); otherwise only the sort
  * passes the step's time span needs are launched.  The rows also advance the
  * store clock after this step.  Call once per step, in step order, also when
- * m_recv is 0. */
+ * m_recv is 0.  recv_info_host NULL (world 1 only: one source): the merge is
+ * planned on the device -- no host read of the rows, the store clock kept in
+ * device memory from then on (a router then takes no host-planned merge:
+ * RL_EINVAL) -- as a per-tile max, one scan block and one gather. */
 int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info,
                    const int64_t* recv_info_host, uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg,
                    int64_t* server_ms, uint32_t* at, void* stream);
