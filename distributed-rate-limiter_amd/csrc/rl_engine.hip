@@ -956,12 +956,13 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         uint32_t* plan = B.ctrl + CTRL_PLAN;
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(B.sk0, B.sv0, B.sk1, B.sv1, m, e->sort_bits - 8, ghist,
                                                        B.status, B.ctrl + CTRL_TILE, e->d_eflags, nullptr, plan,
-                                                       LOC_MAX, e->d_plan);
+                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr);
         const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
         uint32_t* fk = odd ? B.sk0 : B.sk1;
         uint32_t* fv = odd ? B.sv0 : B.sv1;
         // predicted plan: when the batch cannot hold a bucket too large for
-        // LDS, or the last plan the host sees had none, only k_sort_local is
+        // LDS, or the last plan the host sees had none (only batches larger
+        // than LOC_MAX write it: a smaller one fits whatever its keys), only k_sort_local is
         // launched (it sorts a bucket too large for LDS itself, slowly: a
         // misprediction costs time, never a result) -- no LSD passes and no
         // k_segments, which would only find the plan flag and return

@@ -245,8 +245,7 @@ def test_sort_predicted_plan_and_misprediction(rl):
         res = eng.decide(key, ts, n, cfg, sms)
         assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
         pred.append(int(eng.stats().sort_predicted - before))
-    # (batch 0 follows the engine's warm-up batch, whose plan fit)
-    assert pred[1:] == [1, 1, 1, 0, 0, 1]       # batch 3 (hot) mispredicted: loc_sort_big
+    assert pred == [0, 1, 1, 1, 0, 0, 1]        # batch 3 (hot) mispredicted: loc_sort_big
 
 
 def test_single_hot_key_full_batch(rl):
