@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round checkpoint on a GPU box: GPU suite, smoke, bench, rocprofv3 kernel
-# stats + FETCH/WRITE passes (configs[1] and mixed), per-workload survey,
+# stats + FETCH/WRITE passes (configs[1] as the bench runs it, mixed), per-workload survey,
 # then (FULL=1) the gRPC levels and the coalescer e2e levels.
 # Usage: T=<tag> [FULL=1] bash scripts/checkpoint.sh   (outputs: gpurun_out/<tag>_*)
 set -o pipefail
@@ -14,7 +14,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 cat gpurun_out/${T}_smoke.txt
 timeout -k 10 300 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
 cat gpurun_out/${T}_bench.json
-TAG=${T}_zipf BARGS="--steps 10 --warmup 2 --no-cpu-baseline --lat-batches 0" bash scripts/profile.sh > gpurun_out/${T}_prof_zipf.txt 2>&1 || { cat gpurun_out/${T}_prof_zipf.txt; exit 1; }
+TAG=${T}_zipf BARGS="--no-cpu-baseline" bash scripts/profile.sh > gpurun_out/${T}_prof_zipf.txt 2>&1 || { cat gpurun_out/${T}_prof_zipf.txt; exit 1; }
 TAG=${T}_mixed BARGS="--workload mixed --steps 10 --warmup 2 --no-cpu-baseline --lat-batches 0" bash scripts/profile.sh > gpurun_out/${T}_prof_mixed.txt 2>&1 || { cat gpurun_out/${T}_prof_mixed.txt; exit 1; }
 bash scripts/survey.sh > gpurun_out/${T}_survey.txt 2>&1
 cat gpurun_out/${T}_survey.txt
