@@ -620,6 +620,27 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_unpack(uint32_t m, const uin
     }
 }
 
+// one GPU: nothing travels between the owner's results and the sender's
+// unpack, so the caller's outputs come straight from the engine's: request i
+// was received as send slot[i] and decided at position at[slot[i]]
+__global__ __launch_bounds__(RT_BLOCK) void k_route_results_local(uint32_t m, const uint32_t* __restrict__ slot,
+                                                                  const uint32_t* __restrict__ at,
+                                                                  const uint8_t* __restrict__ dec_in,
+                                                                  const int64_t* __restrict__ rem_in,
+                                                                  const int64_t* __restrict__ retry_in,
+                                                                  const int64_t* __restrict__ reset_in,
+                                                                  uint8_t* __restrict__ dec, int64_t* __restrict__ rem,
+                                                                  int64_t* __restrict__ retry,
+                                                                  int64_t* __restrict__ reset) {
+    for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
+        const uint32_t p = at[slot[i]];
+        dec[i] = dec_in[p];
+        rem[i] = rem_in[p];
+        retry[i] = retry_in[p];
+        reset[i] = reset_in[p];
+    }
+}
+
 int grid_for(size_t m) { return (int)std::min<size_t>((m + RT_BLOCK - 1) / RT_BLOCK, 2048); }
 
 }  // namespace
@@ -847,5 +868,19 @@ extern "C" int rl_route_unpack(size_t m, const uint32_t* slot, const rl_route_re
     if (!m) return RL_OK;
     k_route_unpack<<<grid_for(m), RT_BLOCK, 0, (hipStream_t)stream>>>((uint32_t)m, slot, back, decision, remaining,
                                                                       retry_after_ns, reset_at_ns);
+    return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
+}
+
+extern "C" int rl_route_results_local(size_t m, const uint32_t* slot, const uint32_t* at, const uint8_t* decision_in,
+                                      const int64_t* remaining_in, const int64_t* retry_in, const int64_t* reset_in,
+                                      uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns,
+                                      int64_t* reset_at_ns, void* stream) {
+    if (m > (1u << 30) || (m && (!slot || !at || !decision_in || !remaining_in || !retry_in || !reset_in || !decision ||
+                                 !remaining || !retry_after_ns || !reset_at_ns)))
+        return RL_EINVAL;
+    if (!m) return RL_OK;
+    k_route_results_local<<<grid_for(m), RT_BLOCK, 0, (hipStream_t)stream>>>(
+        (uint32_t)m, slot, at, decision_in, remaining_in, retry_in, reset_in, decision, remaining, retry_after_ns,
+        reset_at_ns);
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
 }

@@ -200,6 +200,7 @@ _sig = {
     "rl_route_merge": (C.c_int, [vp, C.c_size_t] + [vp] * 10),
     "rl_route_results": (C.c_int, [C.c_size_t] + [vp] * 7),
     "rl_route_unpack": (C.c_int, [C.c_size_t] + [vp] * 7),
+    "rl_route_results_local": (C.c_int, [C.c_size_t] + [vp] * 11),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -425,6 +426,12 @@ class Router:
         rc = lib.rl_route_unpack(m, slot, back, dec, rem, retry, reset, stream)
         if rc != RL_OK:
             raise EngineError(rc, "rl_route_unpack")
+
+    @staticmethod
+    def results_local(m, slot, at, dec_in, rem_in, retry_in, reset_in, dec, rem, retry, reset, stream):
+        rc = lib.rl_route_results_local(m, slot, at, dec_in, rem_in, retry_in, reset_in, dec, rem, retry, reset, stream)
+        if rc != RL_OK:
+            raise EngineError(rc, "rl_route_results_local")
 
     def sync(self, stream=None) -> int:
         return lib.rl_router_sync(self.h, stream)

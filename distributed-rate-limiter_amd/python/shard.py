@@ -272,13 +272,19 @@ class RoutedPipeline:
             self.decide(tot, p(s["key"]), p(s["ts"]), p(s["n"]), p(s["cfg"]), p(s["sms"]), p(s["dec"]),
                         p(s["rem"]), p(s["retry"]), p(s["reset"]), self._sp(S))
             self._tick("b_decide")
-            self.ops.results(tot, p(s["at"]), p(s["dec"]), p(s["rem"]), p(s["retry"]), p(s["reset"]), p(s["res"]),
-                             self._sp(S))
-            self._tick("b_results")
-            if not self.local:
-                self._a2a(s["back"][:m], s["res"][:tot], sc, rc, self.pg_res)
-            self._tick("b_a2a_res")
-            self.ops.unpack(m, p(s["slot"]), p(s["res"] if self.local else s["back"]), p(dec), p(rem), p(retry), p(reset), self._sp(S))
+            if self.local and hasattr(self.ops, "results_local"):
+                # nothing travels between results and unpack: one pass
+                self.ops.results_local(m, p(s["slot"]), p(s["at"]), p(s["dec"]), p(s["rem"]), p(s["retry"]),
+                                       p(s["reset"]), p(dec), p(rem), p(retry), p(reset), self._sp(S))
+            else:
+                self.ops.results(tot, p(s["at"]), p(s["dec"]), p(s["rem"]), p(s["retry"]), p(s["reset"]),
+                                 p(s["res"]), self._sp(S))
+                self._tick("b_results")
+                if not self.local:
+                    self._a2a(s["back"][:m], s["res"][:tot], sc, rc, self.pg_res)
+                self._tick("b_a2a_res")
+                self.ops.unpack(m, p(s["slot"]), p(s["res"] if self.local else s["back"]), p(dec), p(rem), p(retry),
+                                p(reset), self._sp(S))
             if S is not None:
                 s["ev_done"] = torch.cuda.Event()
                 s["ev_done"].record(S)

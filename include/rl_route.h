@@ -127,6 +127,14 @@ int rl_route_results(size_t m_recv, const uint32_t* at, const uint8_t* decision,
 int rl_route_unpack(size_t m, const uint32_t* slot, const rl_route_res* back, uint8_t* decision,
                     int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns, void* stream);
 
+/* one GPU (nothing exchanged between the two): rl_route_results and
+ * rl_route_unpack in one pass -- the caller's outputs for request i from the
+ * engine's outputs at position at[slot[i]] */
+int rl_route_results_local(size_t m, const uint32_t* slot, const uint32_t* at, const uint8_t* decision_in,
+                           const int64_t* remaining_in, const int64_t* retry_in, const int64_t* reset_in,
+                           uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif
