@@ -102,3 +102,31 @@ def test_routed_pipeline_matches_single_shared_limiter():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_routed_pipeline_world1_local_mode():
+    """world size 1: the pipeline runs no collective and reads nothing back
+    (records and results read in place, merge planned without host rows);
+    the results still equal the one shared limiter, batches out of time order
+    included (CPU restatement of the kernels, oracle as the engine)"""
+    import torch
+
+    import oracle
+    import route_ops
+    import shard
+    sim = oracle.OracleSim(0)
+    for a, L, W in CONFIGS:
+        sim.add_config(a, L, W)
+    pipe = shard.RoutedPipeline(route_ops.NumpyRouteOps(1), route_ops.oracle_decide(sim), 1, 4000, "cpu",
+                                depth=4, lookahead=2)
+    assert pipe.local
+    mine = skewed_rank_batches(1)
+    ins = [tuple(torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else
+                                  (x.view(np.int32) if x.dtype == np.uint32 else x)) for x in bt) for bt in mine]
+    outs = [(torch.empty(b[0].size, dtype=torch.uint8),) + tuple(torch.empty(b[0].size, dtype=torch.int64)
+                                                               for _ in range(3)) for b in mine]
+    pipe.run(ins, outs)
+    exp = route_ops.shared_limiter_expectations([mine], 0, CONFIGS)
+    for ob, eb in zip(outs, exp):
+        for o, e in zip(ob, eb):
+            assert np.array_equal(o.numpy().astype(np.int64), np.asarray(e, np.int64))
