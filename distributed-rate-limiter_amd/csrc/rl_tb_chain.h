@@ -75,6 +75,10 @@ __device__ inline int ch_producer_index(uint32_t wave) {
 }
 constexpr int CH_BLOCK = (CH_NP + 2) * 64;
 constexpr int CH_SERIAL = 64;                          // serial exact steps per round at most
+#ifndef RL_HEAVY_G
+#define RL_HEAVY_G 2
+#endif
+constexpr int HEAVY_G = RL_HEAVY_G;                    // heavy segments per wave claim (k_tb_chain phase 2)
 // conservative scale of the allow/clamp threshold th*P (covers the rounding of
 // th*P and of the bound arithmetic with a wide margin)
 constexpr double CH_YSCALE = 1.0 - 0x1p-28;
@@ -1463,18 +1467,27 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         }
     }
     {
+        // heavy segments, HEAVY_G per claim: every wave's claim is an atomic on
+        // ONE counter, which sustains only ~88 atomics/us -- with one segment
+        // per claim, ten thousand short heavy segments (configs[0]'s keys)
+        // spent longer queueing on the counter than replaying
         uint32_t iters = 0;
+        const uint32_t nhw = nheavy + nwin;
         for (;;) {
-            uint32_t u = 0;
-            if ((threadIdx.x & 63) == 0) u = atomicAdd(&qctr[2], 1u);
-            u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
-            if (u >= nheavy + nwin) break;
-            if (u < nheavy) {
-                const SegRec sg = L.list[0][u];
-                wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
-            } else {
-                const SegRec sg = L.list[2][u - nheavy];
-                wave_win_segment(&win[sk[sg.j0] - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+            uint32_t u0 = 0;
+            if ((threadIdx.x & 63) == 0) u0 = atomicAdd(&qctr[2], (uint32_t)HEAVY_G);
+            u0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0);
+            if (u0 >= nhw) break;
+            const uint32_t u1 = min(u0 + (uint32_t)HEAVY_G, nhw);
+            for (uint32_t u = u0; u < u1; u++) {
+                if (u < nheavy) {
+                    const SegRec sg = L.list[0][u];
+                    wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
+                } else {
+                    const SegRec sg = L.list[2][u - nheavy];
+                    wave_win_segment(&win[sk[sg.j0] - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a,
+                                     eflags);
+                }
             }
         }
     }
