@@ -453,7 +453,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
                           "near_setup_x16": int(dbgw[39]) * 16,
                           # stamps build: the hot chain's exact tiles (cycles, passes)
-                          "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])]},
+                          "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
+                          # batches whose grouping sort ran as k_sort_local alone (predicted plan)
+                          "sort_predicted_batches": int(st.sort_predicted), "batches": int(st.batches)},
         "latency": latency,
         "stamp_ring": stamp_ring,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
