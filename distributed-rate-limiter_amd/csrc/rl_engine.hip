@@ -493,8 +493,11 @@ struct rl_engine {
     hipEvent_t ev_reset = nullptr;    // rl_reset_device: the DEL on `chain` -> the caller's stream
     int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
     size_t zero_bytes = 0;
-    int coop_grid = 96;         // k_tb_chain blocks (one per CU fits its LDS): 96 of 256 CUs, the
-                                // rest run the other batches' grouping and finish (A/B: scripts/ab_grid.sh)
+    int coop_grid = 128;        // k_tb_chain blocks launched (one per CU fits its LDS) ...
+    int coop_base = 96;         // ... of which those past 96 of 256 CUs exit at once unless the batch
+                                // has at least m / coop_light_div light segments: the other CUs run
+                                // the neighbouring batches' grouping and finish (profiles/r3al_ab_replay_grid.txt)
+    uint32_t coop_light_div = 4;
     int probe_grid = 1024;      // k_probe blocks at most
     int perm_grid = 1024;       // k_permute / k_unpermute blocks at most
     uint32_t heavy_min = 32;    // segments this long replay cooperatively
@@ -754,6 +757,8 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     if (const char* v = getenv("RL_HEAVY_MIN")) e->heavy_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_HUGE_MIN")) e->huge_min = (uint32_t)atoi(v);
     if (const char* v = getenv("RL_COOP_GRID")) e->coop_grid = atoi(v);
+    if (const char* v = getenv("RL_COOP_BASE")) e->coop_base = atoi(v);
+    if (const char* v = getenv("RL_COOP_LIGHT_DIV")) e->coop_light_div = (uint32_t)std::max(1, atoi(v));
     if (const char* v = getenv("RL_PROBE_GRID")) e->probe_grid = atoi(v);
     if (const char* v = getenv("RL_PERM_GRID")) e->perm_grid = atoi(v);
     e->stamps = getenv("RL_STAMP_KERNELS") != nullptr;
@@ -1034,11 +1039,13 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (ncfg <= (uint32_t)MAX_LCFG)
         hipExtLaunchKernelGGL(k_tb_chain<true>, dim3(e->coop_grid), dim3(CH_BLOCK), (uint32_t)e->chain_pad[0], c, ev_a, ev_b,
                               0u, kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(), e->d_cfg, ncfg,
-                              e->profile, ps, pre, e->d_eflags, dbg, B.runs);
+                              e->profile, ps, pre, e->d_eflags, dbg, B.runs, (uint32_t)e->coop_base,
+                              m / e->coop_light_div);
     else
         hipExtLaunchKernelGGL(k_tb_chain<false>, dim3(e->coop_grid), dim3(CH_BLOCK), (uint32_t)e->chain_pad[1], c, ev_a, ev_b,
                               0u, kin, lists, segctr + 4, e->win_base, e->d_tb, e->d_win, e->spill(), e->d_cfg, ncfg,
-                              e->profile, ps, pre, e->d_eflags, dbg, B.runs);
+                              e->profile, ps, pre, e->d_eflags, dbg, B.runs, (uint32_t)e->coop_base,
+                              m / e->coop_light_div);
     HIPCHK(e, hipGetLastError());
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 19);
     if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 3);

@@ -1416,7 +1416,8 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
                                                        uint32_t win_base, TbEntry* tb, WinEntry* win, Spill spill,
                                                        const CfgDev* __restrict__ gcfgs, uint32_t ncfg,
                                                        int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
-                                                       uint32_t* dbg, TbRuns runs) {
+                                                       uint32_t* dbg, TbRuns runs, uint32_t grid_base,
+                                                       uint32_t light_min) {
     __shared__ ChainShared sh;
     __shared__ uint32_t s_u;
     __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
@@ -1426,6 +1427,10 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
     }
     const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
     const uint32_t nheavy = L.count[0], nlight = L.count[1], nwin = L.count[2], nhuge = L.count[3];
+    // blocks past grid_base join only a batch with a long light phase (many
+    // distinct keys: every one a serial replay); otherwise they would only
+    // take CUs from the next batch's grouping, which then bounds the step
+    if (blockIdx.x >= grid_base && nlight < light_min) return;
     // timeline (10 ns ticks, low 32 bits): dbg[13] = ~first block start,
     // dbg[14] = last block end, dbg[16/17] = longest segment start / end
     if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
