@@ -129,6 +129,43 @@ def test_merge_single_sorted_source_keeps_order(rl):
     r.close()
 
 
+def test_merge_planned_on_the_device_one_source(rl):
+    """world 1 without host rows (rl_route_merge(..., NULL, ...)): per-tile
+    maxima, one scan block that advances the store clock in device memory, one
+    gather -- the same outputs as the restatement over three steps, batches
+    out of time order and one step whose times go back below the clock; a
+    host-planned merge on that router is then refused"""
+    import torch
+
+    import route_ops
+    m = 25_000
+    rng = np.random.default_rng(17)
+    r = rl.Router(0, 1, m, m)
+    ops = route_ops.NumpyRouteOps(1)
+    s = torch.cuda.current_stream().cuda_stream
+    base = [T0, T0 + 4_000_000_000, T0 + 1_000_000_000]      # step 3 goes back in time
+    for step in range(3):
+        ts = base[step] + rng.integers(0, 3_000_000_000, m).astype(np.int64)   # unsorted, 3 s span
+        rec = np.stack([rng.integers(0, 1 << 62, m), ts, rng.integers(1, 4, m), np.arange(m, dtype=np.int64) << 32],
+                       1)
+        info = np.array([[m, ts.min(), ts.max(), 0]], np.int64)
+        d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
+            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
+             torch.empty(m, dtype=torch.int32, device="cuda")]
+        h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
+            [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
+        rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
+        r.merge(m, rt.data_ptr(), it.data_ptr(), None, *[x.data_ptr() for x in d], s)
+        rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
+        ops.merge(m, rh.data_ptr(), ih.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
+        assert r.sync(s) == rl.RL_OK
+        for a, b in zip(d, h):
+            assert torch.equal(a.cpu(), b)
+    with pytest.raises(rl.EngineError):
+        r.merge(m, rt.data_ptr(), it.data_ptr(), torch.from_numpy(info).data_ptr(), *[x.data_ptr() for x in d], s)
+    r.close()
+
+
 @pytest.mark.parametrize("span_bits", [33, 41])
 def test_merge_wide_time_spans_and_unsorted_sources(rl, span_bits):
     """received times spanning more than 2^32 ns (five and six sort passes),
