@@ -687,16 +687,19 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     auto bail = [&](int code) { int r = code; free_all(e); delete e; return r; };
     if (hipSetDevice(e->device) != hipSuccess) return bail(RL_EDEVICE);
     {
-        // grouping and finish kernels never use RESERVED_CUS CUs (one per 32):
+        // grouping and finish kernels never use the reserved CUs (one per 8):
         // when a replay is launched those are free, so its first blocks -- the
         // longest segments -- start at once instead of waiting for a CU that
         // the other two streams' blocks have left empty
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, e->device) != hipSuccess) return bail(RL_EDEVICE);
         const int ncu = prop.multiProcessorCount;
+        int every = 8;    // one reserved CU per `every` (0: none); one per 32 (round 2) held the
+                          // grouping of the uniform workloads back: profiles/r3aq_ab_reserved_cus.txt
+        if (const char* v = getenv("RL_RESERVE_EVERY")) every = atoi(v);
         std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
         for (int c = 0; c < ncu; c++)
-            if (c % 32 != 31 || ncu < 64) mask[c / 32] |= 1u << (c % 32);
+            if (every <= 0 || c % every != every - 1 || ncu < 64) mask[c / 32] |= 1u << (c % 32);
         if (hipExtStreamCreateWithCUMask(&e->front, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
             hipExtStreamCreateWithCUMask(&e->tail, (uint32_t)mask.size(), mask.data()) != hipSuccess)
             return bail(RL_EDEVICE);
