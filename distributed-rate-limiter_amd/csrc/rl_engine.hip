@@ -550,13 +550,16 @@ static int fail(rl_engine* e, int code, const std::string& msg) {
     } while (0)
 
 // versioned output structs (include/rl_engine.h): the caller's struct_size
-// bounds what is written; a size smaller than the header field is rejected
+// bounds what is written, and struct_size comes back as the bytes actually
+// filled in (min(caller's, library's)), so a caller built against a newer
+// header sees which trailing fields this library knows; a size smaller than
+// the header field is rejected
 template <class T>
 static int copy_out(T* dst, T src) {
     if (dst->struct_size < 8) return RL_EINVAL;
-    const uint32_t n = dst->struct_size;
+    const uint32_t n = (uint32_t)std::min<size_t>(dst->struct_size, sizeof(T));
     src.struct_size = n;
-    memcpy(dst, &src, std::min<size_t>(n, sizeof(T)));
+    memcpy(dst, &src, n);
     return RL_OK;
 }
 

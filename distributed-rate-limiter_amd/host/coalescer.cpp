@@ -397,6 +397,25 @@ void Coalescer::drop_locked(Sub* s, int code) {
     notify_locked(s);
 }
 
+void Coalescer::truncate_locked(Sub* s, int code) {
+    // part of it was launched (applied, as an EVAL already sent); the part not
+    // yet launched is dropped unapplied, so nothing is sent after its context
+    // ended.  taken = m stops the submitter; it pops the submission when it
+    // reaches the head of the queue
+    const size_t rest = s->m - s->taken;
+    if (rest == 0) return;
+    pending_ -= rest;
+    if (s->op == OP_REQ) (code == RL_ECANCELED ? st_.cancelled : st_.expired) += rest;
+    s->taken = s->m;
+    s->left -= rest;
+    if (s->left == 0 && !s->done) {
+        s->done = true;
+        s->done_ns = steady_ns();
+        if (s->waiting) s->cv.notify_all();
+        notify_locked(s);
+    }
+}
+
 void Coalescer::maybe_free_locked(Sub* s) {
     if (s->waited && !s->in_queue && s->inflight == 0) put_sub(s);
 }
@@ -409,7 +428,10 @@ int Coalescer::Cancel(uint64_t ticket) {
     if (s->done) return RL_OK;
     s->cancelled = true;
     if (s->taken == 0) drop_locked(s, RL_ECANCELED);
-    else if (s->waiting) s->cv.notify_all();
+    else {
+        truncate_locked(s, RL_ECANCELED);
+        if (s->waiting) s->cv.notify_all();
+    }
     return RL_OK;
 }
 
@@ -429,8 +451,10 @@ int Coalescer::Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* 
         }
         const int64_t now = steady_ns();
         if (s->deadline && now >= s->deadline) {
-            // not launched: never applied; launched: applied, results discarded
+            // not launched: never applied; launched: applied, results discarded,
+            // and what was not launched yet never will be
             if (s->taken == 0) drop_locked(s, RL_EDEADLINE);
+            else truncate_locked(s, RL_EDEADLINE);
             code = RL_EDEADLINE;
             break;
         }
@@ -681,9 +705,13 @@ void Coalescer::submitter() {
                     continue;
                 }
                 if (sub->op != OP_REQ) break;
-                if (sub->taken == 0 && (sub->cancelled || (sub->deadline && sub->deadline <= now))) {
-                    // its context ended before it was sent: never applied
-                    drop_locked(sub, sub->cancelled ? RL_ECANCELED : RL_EDEADLINE);
+                if (sub->taken < sub->m && (sub->cancelled || (sub->deadline && sub->deadline <= now))) {
+                    // its context ended before (the rest of) it was sent: that part is never applied
+                    if (sub->taken == 0) drop_locked(sub, sub->cancelled ? RL_ECANCELED : RL_EDEADLINE);
+                    else truncate_locked(sub, sub->cancelled ? RL_ECANCELED : RL_EDEADLINE);
+                }
+                if (sub->dropped || sub->taken == sub->m) {
+                    // dropped, or the rest of a split submission truncated: nothing left to launch
                     queue_.pop_front();
                     sub->in_queue = false;
                     maybe_free_locked(sub);
@@ -912,9 +940,9 @@ static int table_op(rl_coalescer* c, rlc::Op op, int64_t now_ms, uint64_t tb, ui
     rl_table_info info{};
     rc = c->c->Wait(t, -1, nullptr, nullptr, nullptr, nullptr, nullptr, &info);
     if (out && rc == RL_OK) {
-        const uint32_t n = out->struct_size;
+        const uint32_t n = (uint32_t)std::min<size_t>(out->struct_size, sizeof info);   // bytes filled in
         info.struct_size = n;
-        memcpy(out, &info, std::min<size_t>(n, sizeof info));
+        memcpy(out, &info, n);
     }
     return rc;
 }
@@ -933,8 +961,8 @@ extern "C" int rl_coalescer_gc(rl_coalescer* c, int64_t now_ms, uint64_t tb_capa
 extern "C" int rl_coalescer_get_stats(rl_coalescer* c, rl_coalescer_stats* out) {
     if (!c || !out || out->struct_size < 8) return RL_EINVAL;
     rl_coalescer_stats s = c->c->Stats();
-    const uint32_t n = out->struct_size;
+    const uint32_t n = (uint32_t)std::min<size_t>(out->struct_size, sizeof s);   // bytes filled in
     s.struct_size = n;
-    memcpy(out, &s, std::min<size_t>(n, sizeof s));
+    memcpy(out, &s, n);
     return RL_OK;
 }

@@ -147,6 +147,9 @@ private:
     void completer();
     // drop a submission none of whose requests was launched: done, unapplied
     void drop_locked(Sub* s, int code);
+    // a submission split across launches whose context ended: drop the part
+    // not launched yet (never applied); the launched part completes as usual
+    void truncate_locked(Sub* s, int code);
     // a submission became done (lock held): the completion callback
     void notify_locked(Sub* s) {
         if (notify_ && s->tag) notify_(notify_user_, s->first, s->tag);

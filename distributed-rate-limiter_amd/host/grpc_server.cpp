@@ -172,16 +172,23 @@ int64_t parse_timeout(std::string_view v) {
         if (v[i] < '0' || v[i] > '9') return -1;
         x = x * 10 + (v[i] - '0');
     }
+    int64_t unit;
     switch (v.back()) {
-        case 'H': return x * 3600 * 1000000000LL;
-        case 'M': return x * 60 * 1000000000LL;
-        case 'S': return x * 1000000000LL;
-        case 'm': return x * 1000000LL;
-        case 'u': return x * 1000LL;
-        case 'n': return x;
+        case 'H': unit = 3600 * 1000000000LL; break;
+        case 'M': unit = 60 * 1000000000LL; break;
+        case 'S': unit = 1000000000LL; break;
+        case 'm': unit = 1000000LL; break;
+        case 'u': unit = 1000LL; break;
+        case 'n': unit = 1; break;
         default: return -1;
     }
+    // the header comes from the network: saturate instead of overflowing
+    // (99999999H is ~1.1e4 years of nanoseconds)
+    return x > INT64_MAX / unit ? INT64_MAX : x * unit;
 }
+
+// a timeout this long (~100 years, e.g. grpc-go's 2562047H maximum) is no deadline
+constexpr int64_t NO_DEADLINE_NS = 100LL * 365 * 24 * 3600 * 1000000000LL;
 
 // ---------------------------------------------------------------------------
 // server state
@@ -462,7 +469,9 @@ void collect(Io* io, uint64_t ticket) {
 void submit_rpc(Io* io, Conn* c, Stream* st, Rpc&& rpc, size_t m, const uint64_t* key, const int64_t* ts,
                 const int64_t* n, const uint32_t* cfg) {
     Server* s = io->srv;
-    rpc.deadline = st->timeout_ns >= 0 ? std::max<int64_t>(1, rlc::steady_ns() + st->timeout_ns) : 0;
+    rpc.deadline = st->timeout_ns >= 0 && st->timeout_ns < NO_DEADLINE_NS
+                       ? std::max<int64_t>(1, rlc::steady_ns() + st->timeout_ns)   // no overflow below the bound
+                       : 0;
     uint64_t ticket = 0;
     int rc;
     if (rpc.kind == K_RESET) rc = s->co->SubmitOp(rlc::OP_RESET, key[0], ts[0], cfg[0], 0, 0, 0, &ticket, io);
@@ -933,8 +942,8 @@ extern "C" int rl_grpc_server_get_stats(rl_grpc_server* g, rl_grpc_stats* out) {
     r.decisions = s.n_dec;
     r.errors = s.n_err;
     r.cancelled = s.n_cancel;
-    const uint32_t n = out->struct_size;
+    const uint32_t n = (uint32_t)std::min<size_t>(out->struct_size, sizeof r);   // bytes filled in
     r.struct_size = n;
-    memcpy(out, &r, std::min<size_t>(n, sizeof r));
+    memcpy(out, &r, n);
     return RL_OK;
 }

@@ -277,6 +277,34 @@ def test_cancel_before_and_after_launch(rl, oracle_mod):
     assert [a[2] for a in be.applied] == [5, 1, 1]
 
 
+@pytest.mark.parametrize("how", ["cancel", "deadline"])
+def test_split_submission_context_end_drops_the_rest(rl, oracle_mod, how):
+    """a submission larger than max_batch, split across launches, whose context
+    ends after its first launch: the launched part is applied (an EVAL already
+    sent), the part not launched yet never reaches the store"""
+    be = GatedOracle(oracle_mod, CONFIGS[:1])
+    co = rl.Coalescer(be.batch, max_batch=8, max_in_flight=1)
+    be.gate.clear()
+    m = 20
+    keys = np.full(m, 5, np.uint64)
+    ts = T0 + np.arange(m, dtype=np.int64)
+    dl = rl.now_ns() + 40_000_000 if how == "deadline" else 0
+    t = co.submit(keys, ts, np.ones(m, np.int64), np.zeros(m, np.uint32), deadline_ns=dl)
+    assert be.entered.wait(10)                      # the first 8 are on the "GPU"
+    if how == "cancel":
+        assert co.cancel(t) == 0
+        assert co.wait(t, 1)[0] == rl.RL_ECANCELED
+    else:
+        assert co.wait(t, 1)[0] == rl.RL_EDEADLINE
+    be.gate.set()
+    rc, (d, rem, _, _) = co.decide(5, T0 + 100, 1, 0)
+    assert rc == 0 and d == rl.ALLOWED and rem == 20 - 8 - 1   # the other 12 never happened
+    st = co.stats()
+    co.close()
+    assert [a[0] for a in be.applied] == [5] * 9
+    assert (st.cancelled if how == "cancel" else st.expired) == 12
+
+
 def test_cancelled_context_before_the_call(rl, oracle_mod):
     """interface_test.go:267-275: Allow with an already-cancelled context
     returns an error; the store is untouched"""
@@ -480,6 +508,14 @@ def test_abi_struct_sizes_are_checked(rl):
     assert st.batches == 12345 and st.struct_size == 24
     st.struct_size = 0
     assert rl.lib.rl_coalescer_get_stats(co.h, Cc.byref(st)) == rl.RL_EINVAL
+    # a newer caller (struct larger than the library's): struct_size comes back
+    # as the bytes the library filled in, and the trailing bytes are untouched
+    big = (Cc.c_uint8 * (Cc.sizeof(rl.rl_coalescer_stats) + 64))()
+    Cc.memset(big, 0xAB, Cc.sizeof(big))
+    Cc.cast(big, Cc.POINTER(Cc.c_uint32))[0] = Cc.sizeof(big)
+    assert rl.lib.rl_coalescer_get_stats(co.h, Cc.cast(big, Cc.POINTER(rl.rl_coalescer_stats))) == 0
+    assert Cc.cast(big, Cc.POINTER(Cc.c_uint32))[0] == Cc.sizeof(rl.rl_coalescer_stats)
+    assert bytes(big[Cc.sizeof(rl.rl_coalescer_stats):]) == b"\xab" * 64
     co.close()
     bad = rl.rl_opts(max_batch=16)
     bad.struct_size = 16

@@ -98,6 +98,66 @@ def test_native_allow_n_reset_and_errors(native):
     assert srv.st.AllowN(srv.a.AllowNRequest(limiter="tb", key="k", n=5)).remaining == 0
 
 
+def _raw_h2_unary(port, path, body, extra_headers):
+    """one gRPC unary call over a bare HTTP/2 connection (HPACK literals, no
+    Huffman): lets a test send header values a gRPC client library never
+    would; returns the response message, None when the call ended without
+    one (an error status)"""
+    import socket
+    import struct
+
+    def frame(ftype, flags, sid, payload):
+        return struct.pack(">I", len(payload))[1:] + bytes([ftype, flags]) + struct.pack(">I", sid) + payload
+
+    def lit(name, value):        # literal header field without indexing, new name
+        n, v = name.encode(), value.encode()
+        assert len(n) < 127 and len(v) < 127
+        return b"\x00" + bytes([len(n)]) + n + bytes([len(v)]) + v
+
+    hdrs = [(":method", "POST"), (":scheme", "http"), (":path", path), (":authority", "127.0.0.1"),
+            ("content-type", "application/grpc"), ("te", "trailers")] + extra_headers
+    block = b"".join(lit(k, v) for k, v in hdrs)
+    msg = b"\x00" + struct.pack(">I", len(body)) + body
+    s = socket.create_connection(("127.0.0.1", port), timeout=10)
+    s.sendall(b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n" + frame(4, 0, 0, b"") + frame(1, 4, 1, block) +
+              frame(0, 1, 1, msg))
+    buf = b""
+    body_out, ended = None, False
+    while not ended:
+        chunk = s.recv(65536)
+        assert chunk, "connection closed before the trailers"
+        buf += chunk
+        while len(buf) >= 9:
+            ln = int.from_bytes(buf[:3], "big")
+            if len(buf) < 9 + ln:
+                break
+            ftype, flags, sid, payload = buf[3], buf[4], int.from_bytes(buf[5:9], "big"), buf[9:9 + ln]
+            buf = buf[9 + ln:]
+            if ftype == 4 and not flags & 1:
+                s.sendall(frame(4, 1, 0, b""))          # SETTINGS ack
+            if sid == 1 and ftype == 0 and len(payload) >= 5:
+                body_out = payload[5:]                 # the response message (a DATA frame)
+            if sid == 1 and ftype in (0, 1) and flags & 1:
+                ended = True                           # END_STREAM: the trailers (HPACK, not decoded here)
+    s.close()
+    return body_out
+
+
+@pytest.mark.parametrize("timeout", ["2562047H", "99999999H", "99999999M"])
+def test_native_huge_grpc_timeouts_are_no_deadline(native, timeout):
+    """grpc-timeout values whose nanoseconds overflow int64 (grpc-go's
+    2562047H maximum, 8-digit hour counts) saturate to no deadline instead of
+    expiring the RPC at once (or overflowing)"""
+    srv, _ = native
+    body = srv.a.AllowRequest(limiter="fw", key="long-deadline-" + timeout).SerializeToString()
+    out = _raw_h2_unary(srv.srv.port, "/ratelimiter.v1.RateLimiter/Allow", body, [("grpc-timeout", timeout)])
+    assert out is not None, "the RPC ended without a response (deadline applied at once)"
+    r = srv.a.AllowResponse.FromString(out)
+    assert r.allowed and r.remaining == 4
+    # and a tiny one still expires (the deadline is applied when it fits)
+    assert srv.st.Allow(srv.a.AllowRequest(limiter="fw", key="after"), timeout=5).allowed
+
+
 def test_native_decisions_equal_the_oracle(native):
     """a random mix of unary and batched RPCs over every limiter == the oracle
     replaying the same requests at the server's clock readings"""
