@@ -469,7 +469,8 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
 
 def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     """every rank draws requests from the whole key space; the native routed
-    pipeline (include/rl_route.h) moves them to their owners and back"""
+    pipeline (include/rl_route.h) moves them to their owners and back in
+    fixed-capacity buckets, with no host read in the step"""
     import torch
     import torch.distributed as dist
 
@@ -484,68 +485,66 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     del host
     algs = {a for a, _, _ in gen.configs}
     tb_cap, win_cap = KEYSPACE[workload]
+    # bucket capacity per peer: a uniform hash partition needs ~m / world plus
+    # a margin; a Zipf hot key lands on one owner (12.4 % of every rank's
+    # batch at s = 1.1), so that workload gets twice the share
+    slack = float(os.environ.get("RL_ROUTE_SLACK", "0")) or (2.0 if workload == "tb_zipf" else 1.25)
+    cap = m if world == 1 else min(m, int(np.ceil(slack * m / world)))
+    router = rl_amd.Router(local_rank, world, m, cap)
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=tb_cap, win_capacity=win_cap,
-                        max_batch=min(world, 2) * m, device=local_rank, flags=0)
+                        max_batch=world * router.capacity, device=local_rank, flags=0)
     for a, L, W in gen.configs:
         eng.register(a, L, W)
-
-    def decide(mm, key, ts, n, cfg, sms, dec, rem, retry, reset, stream):
-        eng.decide_device(mm, key, ts, n, cfg, sms, dec, rem, retry, reset, None, stream)
-
-    router = rl_amd.Router(local_rank, world, m, world * m)
-    pipe = shard.RoutedPipeline(router, decide, world, m, dev, pg_req=None, pg_res=pg_res,
-                                depth=int(os.environ.get("RL_ROUTE_DEPTH", "6")),
-                                lookahead=int(os.environ.get("RL_ROUTE_LOOKAHEAD", "2")))
+    exchange = world > 1 or args.route_exchange
+    pipe = shard.RoutedPipeline(router, eng.decide_routed, world, m, dev, pg_req=None, pg_res=pg_res,
+                                depth=int(os.environ.get("RL_ROUTE_DEPTH", "4")), exchange=exchange)
     outs = [(torch.empty(m, dtype=torch.uint8, device=dev),) +
             tuple(torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)) for _ in range(pipe.depth)]
-    recv = []
     pipe.run(ins[:args.warmup], [outs[b % pipe.depth] for b in range(args.warmup)])
     torch.cuda.synchronize()
     for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
         if rc != 0:
-            raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}")
+            raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}"
+                             + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
     eng.set_timing(0 if os.environ.get("RL_BENCH_NO_TIMING") else 1)
     eng.stage_times()
     dist.barrier()
     torch.cuda.synchronize()
-    pipe.wait_s = 0.0
-    pipe.host_prof = {}
     t0 = time.perf_counter()
-    pipe.run(ins[args.warmup:], [outs[b % pipe.depth] for b in range(args.steps)],
-             done=lambda b, S: recv.append(pipe.last_recv))
+    pipe.run(ins[args.warmup:], [outs[b % pipe.depth] for b in range(args.steps)])
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
         if rc != 0:
-            raise SystemExit(f"{what} error during timed region: {rc} {eng.last_error()}")
+            raise SystemExit(f"{what} error during timed region: {rc} {eng.last_error()}"
+                             + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
     stage_ms, nbat = eng.stage_times()
     st = eng.stats()
     eng.set_timing(0)
-    tt = torch.tensor([elapsed, float(max(recv)), float(sum(recv))], dtype=torch.float64, device=dev)
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     agg = [torch.zeros_like(tt) for _ in range(world)]
     dist.all_gather(agg, tt)
-    agg = torch.stack(agg).cpu().numpy()
-    elapsed = float(agg[:, 0].max())
-    mean_recv = float(np.mean(recv))
-    roof, _ = roofline_of(stage_ms[3] / nbat, algs, int(st.last_segments), int(round(mean_recv)), workload)
+    elapsed = float(torch.stack(agg).max().cpu())
+    # a hash partition: every owner receives ~m requests per step
+    roof, _ = roofline_of(stage_ms[3] / nbat, algs, int(st.last_segments), m, workload)
     res = {
         "value": args.steps * m * world / elapsed,
         "ms_per_step": elapsed / args.steps * 1e3,
         "workload": WORKLOAD_DESC[workload],
-        "ingress": f"routed: owner = hash(key) mod {world}, RCCL all-to-all of 32-B request records and "
-                   f"32-B results over xGMI (include/rl_route.h)",
+        "ingress": (f"routed: owner = hash(key) mod {world}; per peer a fixed-capacity bucket of "
+                    f"{router.capacity} 32-B request records and one of 32-B results, moved by equal-split "
+                    f"RCCL all-to-alls over xGMI" + ("" if exchange else " (world 1: buckets read in place)")
+                    + "; merge and engine sized on the device, no host read in the step (include/rl_route.h)"),
         "batch": m,
-        "received_per_step": {"mean_over_ranks": float(agg[:, 2].sum() / world / args.steps),
-                              "max_rank_step": float(agg[:, 1].max())},
-        "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3}
-        | {k: v / args.steps * 1e3 for k, v in pipe.host_prof.items()},
+        "bucket_capacity": router.capacity,
+        "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
         "roofline": roof,
     }
+    del pipe, outs, ins
     eng.close()
     router.close()
-    del pipe, outs, ins
     rl_amd.release_dedicated_streams()
     return res
 
@@ -566,6 +565,8 @@ def main():
     ap.add_argument("--ingress", default=None, choices=["routed", "sharded"],
                     help="N > 1: routed (default; RCCL all-to-all to the key's owner) or sharded (replicas)")
     ap.add_argument("--no-secondary", action="store_true", help="N > 1: skip the secondary measurements")
+    ap.add_argument("--route-exchange", action="store_true",
+                    help="--ingress routed at N = 1: run the loopback all-to-alls too (the N > 1 step's work)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="cpu_baseline requests per host core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
@@ -655,7 +656,7 @@ def main():
                             else "integer key ids")},
         "roofline": res["roofline"],
     }
-    for k in ("unique_keys_per_batch", "batches_in_flight", "received_per_step", "host_ms_per_step"):
+    for k in ("unique_keys_per_batch", "batches_in_flight", "bucket_capacity", "host_ms_per_step"):
         if k in res:
             out["config"][k] = res[k]
     for k in ("replay_detail", "latency", "stages_ms_per_batch", "stamp_ring"):

@@ -25,6 +25,7 @@
 
 #include "../../include/rl_engine.h"
 #include "../../include/rl_keyhash.h"
+#include "../../include/rl_route.h"
 #include "rl_replay.h"
 #include "rl_semantics.h"
 #include "rl_sort.h"
@@ -96,6 +97,17 @@ __global__ void k_init_spill(SpillEntry* t, uint64_t n) {
 
 constexpr int PROBE_BLOCK = 256;
 
+// A batch the routing layer merged (include/rl_route.h): request p is
+// rec[order[p]] (its store clock in the server-clock array), p < *count --
+// a size in device memory, so the grid is sized for the caller's bound and
+// every kernel reads the actual size -- and its result goes to res[order[p]]
+struct RouteIn {
+    const rl_route_rec* rec;
+    const uint32_t* order;
+    const uint32_t* count;
+    rl_route_res* res;
+};
+
 // find-or-insert one request's key: its global slot (token-bucket table
 // first, then the window table at win_base), or invalid_key when the request
 // is not executed (n <= 0, unknown config, reserved key, table full)
@@ -121,13 +133,17 @@ __device__ inline uint32_t probe_request(uint64_t k, uint32_t c, int64_t nn, con
 // (inputs, then every first table probe) before resolving any: the kernel is
 // latency-bound on random table reads, and this keeps PROBE_R of them in
 // flight per thread instead of one.
-template <int PROBE_R, bool XS>
+// RT: the routed batch of RouteIn (the records read in merge order; XS, the
+// store clock per request, is then always given).
+template <int PROBE_R, bool XS, bool RT = false>
 __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     uint32_t m, const uint64_t* __restrict__ key, const int64_t* __restrict__ n,
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
     uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
     uint32_t* __restrict__ sk, uint32_t* ghist, int passes, uint32_t shifts, ReqArgs a,
-    ReqRec<XS>* __restrict__ rec, uint32_t* eflags) {
+    ReqRec<XS>* __restrict__ rec, uint32_t* eflags, RouteIn ri) {
+    static_assert(!RT || XS, "a routed batch carries its store clock");
+    if (RT) m = min(m, *ri.count);
     __shared__ uint32_t lh[4][RADIX];
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
@@ -142,10 +158,19 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
         for (int r = 0; r < PROBE_R; r++) {   // inputs
             const uint32_t i = i0 + r * PROBE_BLOCK;
             const bool v = i < m;
-            k[r] = v ? key[i] : EMPTY_KEY;
-            c[r] = v ? cfg[i] : 0u;
-            nn[r] = v ? n[i] : 0;
-            t[r] = v ? a.ts[i] : 0;
+            if (RT) {
+                rl_route_rec q{};
+                if (v) q = ri.rec[ri.order[i]];
+                k[r] = v ? q.key : EMPTY_KEY;
+                c[r] = q.cfg;
+                nn[r] = q.n;
+                t[r] = q.ts;
+            } else {
+                k[r] = v ? key[i] : EMPTY_KEY;
+                c[r] = v ? cfg[i] : 0u;
+                nn[r] = v ? n[i] : 0;
+                t[r] = v ? a.ts[i] : 0;
+            }
             sms[r] = v && XS ? a.sms[i] : 0;
         }
 #pragma unroll
@@ -361,6 +386,27 @@ __global__ void k_table_keys(const TbEntry* tb, uint64_t ntb, const WinEntry* wi
     }
 }
 
+// results of a routed batch: one 32-byte result record per request at its
+// receive index (the send layout of the result all-to-all)
+__global__ __launch_bounds__(256) void k_unpermute_routed(const uint32_t* __restrict__ sk,
+                                                          const uint32_t* __restrict__ sv, uint32_t m,
+                                                          uint32_t invalid_key, const CfgDev* __restrict__ cfgs,
+                                                          ReqArgs sorted, RouteIn ri) {
+    m = min(m, *ri.count);
+    for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+        const uint32_t k0 = sk[j];
+        const uint32_t p = sv[j];
+        uint8_t dec = DEC_INVALID;   // rejected by k_probe (n <= 0, unknown config or key, table full)
+        int64_t rem = 0, retry = 0, reset = 0;
+        double tok = 0.0;
+        if (k0 != invalid_key) {
+            dec = sorted.dec[j];
+            finish_result(dec, sorted.tok[j], sorted.ts[j], sorted.n[j], cfgs[sorted.cfg[j]], rem, retry, reset, tok);
+        }
+        ri.res[ri.order[p]] = rl_route_res{(int64_t)dec, rem, retry, reset};
+    }
+}
+
 // diagnostic timestamp (10 ns ticks) into *w
 __global__ void k_stamp(uint32_t* w) { *w = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
@@ -507,6 +553,7 @@ struct rl_engine {
     // GROUP_LDS bytes at least) then never share a CU with a chain
     size_t chain_pad[2] = {0, 0};
     uint32_t* d_eflags = nullptr;
+    uint32_t* d_zero = nullptr;       // a device word holding 0 (warm-up of the routed kernels)
     unsigned long long* d_count = nullptr;   // table counts / GC counters (rl_table_info_get, rl_table_gc)
     unsigned long long* h_count = nullptr;   // pinned host copy
     // the grouping sort's last plan (1: every MSD bucket fit LDS), written by
@@ -629,6 +676,7 @@ static void free_all(rl_engine* e) {
     (void)hipFree(e->d_spill);
     for (auto& B : e->set) free_set(B);
     (void)hipFree(e->d_eflags);
+    (void)hipFree(e->d_zero);
     (void)hipFree(e->d_count);
     if (e->h_count) (void)hipHostFree(e->h_count);
     if (e->h_plan) (void)hipHostFree(e->h_plan);
@@ -730,6 +778,7 @@ extern "C" int rl_engine_create(const rl_opts* o, rl_engine** out) {
     ok &= hipMalloc(&e->d_spill, sizeof(SpillEntry) * e->spill_cap) == hipSuccess;
     for (auto& B : e->set) ok = ok && alloc_set(B, M, e->zero_bytes, status_words);
     ok &= hipMalloc(&e->d_eflags, 4) == hipSuccess;
+    ok &= hipMalloc(&e->d_zero, 4) == hipSuccess && hipMemset(e->d_zero, 0, 4) == hipSuccess;
     ok &= hipMalloc(&e->d_count, 8 * sizeof(unsigned long long)) == hipSuccess;
     ok &= hipHostMalloc(&e->h_count, 8 * sizeof(unsigned long long), hipHostMallocDefault) == hipSuccess;
     ok &= hipHostMalloc(&e->h_plan, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
@@ -897,10 +946,13 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     return RL_OK;
 }
 
+// ri (nullable): a routed batch (RouteIn), at most m requests, its size in
+// device memory; its inputs come from `s` (the merge)
 static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool inputs_ready,
-                     const KeyBytes* kb = nullptr) {
+                     const KeyBytes* kb = nullptr, const RouteIn* ri = nullptr) {
     if (m == 0) return RL_OK;
-    if (m <= e->small_max && !e->timing) return run_small(e, m, a, s, inputs_ready, kb);
+    if (m <= e->small_max && !e->timing && !ri) return run_small(e, m, a, s, inputs_ready, kb);
+    const uint32_t* mdev = ri ? ri->count : nullptr;
     BatchSet& B = e->set[e->next_set];
     e->last_set = e->next_set;
     e->next_set = (e->next_set + 1) % NSETS;
@@ -938,16 +990,22 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // the MSD histogram is used, so the probe counts that pass only
     const bool pred_local = e->sort_passes > 1 && (m <= LOC_MAX || *(volatile uint32_t*)e->h_plan == 1u);
     const int hist_passes = pred_local ? 1 : e->sort_passes;
-    if (xs)
+    const RouteIn rin = ri ? *ri : RouteIn{};
+    if (ri)
+        k_probe<1, true, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
+            m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
+            e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin);
+    else if (xs)
         k_probe<1, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<true>*>(B.rec), e->d_eflags);
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin);
     else
         k_probe<1, false><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<false>*>(B.rec), e->d_eflags);
+            static_cast<ReqRec<false>*>(B.rec), e->d_eflags, rin);
     if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
@@ -957,7 +1015,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
     if (P <= 1) {
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
-                                                       B.ctrl + CTRL_TILE, e->d_eflags);
+                                                       B.ctrl + CTRL_TILE, e->d_eflags, nullptr, nullptr, 0, nullptr,
+                                                       mdev);
         kin = B.sk1;
         vin = B.sv1;
     } else {
@@ -967,7 +1026,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         uint32_t* plan = B.ctrl + CTRL_PLAN;
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(B.sk0, B.sv0, B.sk1, B.sv1, m, e->sort_bits - 8, ghist,
                                                        B.status, B.ctrl + CTRL_TILE, e->d_eflags, nullptr, plan,
-                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr);
+                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr, mdev);
         const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
         uint32_t* fk = odd ? B.sk0 : B.sk1;
         uint32_t* fv = odd ? B.sv0 : B.sv1;
@@ -988,7 +1047,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         for (int p = 1; p < P && !pred_local; p++) {
             uint32_t* status = B.status + (size_t)p * e->max_tiles * RADIX;
             k_sort_pass<false><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 8 * (p - 1), ghist + p * RADIX,
-                                                            status, B.ctrl + CTRL_TILE + p, e->d_eflags, plan);
+                                                            status, B.ctrl + CTRL_TILE + p, e->d_eflags, plan, nullptr,
+                                                            0, nullptr, mdev);
             std::swap(kin, kout);
             std::swap(vin, vout);
         }
@@ -1003,7 +1063,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     int sgrid = (int)std::min<uint32_t>((m + SEG_TILE - 1) / SEG_TILE, 2048);
     if (!pred_local)
         k_segments<<<sgrid, 256, GROUP_LDS, f>>>(kin, m, e->invalid_key, e->win_base, e->heavy_min, huge_min, lists,
-                                                 P > 1 ? B.ctrl + CTRL_PLAN : nullptr);
+                                                 P > 1 ? B.ctrl + CTRL_PLAN : nullptr, mdev);
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     // (the server clock only when the caller gave one: else floor(ts / 1e6) where it is read)
     ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, nullptr, nullptr, nullptr,
@@ -1017,11 +1077,11 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (xs)
         hipExtLaunchKernelGGL(k_permute<true>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre);
+                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre, mdev);
     else
         hipExtLaunchKernelGGL(k_permute<false>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<false>*>(B.rec), a.n, ps, pre);
+                              e->d_cfg, e->profile, static_cast<const ReqRec<false>*>(B.rec), a.n, ps, pre, mdev);
     if (tall) (void)hipEventRecord(ev[3], f);
     if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 1);
     if (!bind_front) HIPCHK(e, hipEventRecord(B.front_done, f));
@@ -1072,7 +1132,10 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 4);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
-    if (m <= UP_MAX) {
+    if (ri) {
+        // a routed batch: one result record per request at its receive index
+        k_unpermute_routed<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->d_cfg, ps, *ri);
+    } else if (m <= UP_MAX) {
         // results to the caller's order through arrival-index buckets: no
         // scattered partial-line stores
         k_unpermute_bucket<<<(m + 256 * UP_ITEMS - 1) / (256 * UP_ITEMS), 256, GROUP_LDS, t>>>(
@@ -1116,6 +1179,13 @@ static int warm_up(rl_engine* e) {
         ReqArgs ax = a;
         ax.sms = e->d_sms;
         const int r = run_batch(e, mb, ax, s, false);
+        if (r != RL_OK) return r;
+    }
+    {   // the routed path's kernels (k_probe<.., true>, k_unpermute_routed) on a
+        // batch whose device size is 0: every kernel returns at once
+        ReqArgs ar{nullptr, nullptr, nullptr, nullptr, e->d_sms, nullptr, nullptr, nullptr, nullptr, nullptr};
+        const RouteIn ri{nullptr, nullptr, e->d_zero, nullptr};
+        const int r = run_batch(e, mb, ar, s, false, nullptr, &ri);
         if (r != RL_OK) return r;
     }
     // the table count / GC / key listing kernels, on empty ranges: a server's
@@ -1173,6 +1243,20 @@ extern "C" int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* ke
         if (r != RL_OK) return r;
     }
     return RL_OK;
+}
+
+extern "C" int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
+                                       const uint32_t* order, const int64_t* server_ms, rl_route_res* res,
+                                       void* stream) {
+    if (!e || !count || (m_max && (!recv || !order || !server_ms || !res))) return RL_EINVAL;
+    if (m_max > e->max_batch) return fail(e, RL_EINVAL, "routed batch bound above max_batch");
+    if (!m_max) return RL_OK;
+    (void)hipSetDevice(e->device);
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    // the server-clock array is the routed records' store clock (always given)
+    ReqArgs a{nullptr, nullptr, nullptr, nullptr, server_ms, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const RouteIn ri{recv, order, count, res};
+    return run_batch(e, (uint32_t)m_max, a, s, false, nullptr, &ri);
 }
 
 extern "C" int rl_decide_batch_keys_device(rl_engine* e, size_t m, const uint8_t* key_bytes, uint64_t nbytes,

@@ -408,8 +408,10 @@ __device__ inline uint32_t seg_skew(uint32_t i) { return i + (i >> 4); }   // LD
 
 __global__ __launch_bounds__(256) void k_segments(const uint32_t* __restrict__ sk, uint32_t m,
                                                   uint32_t invalid_key, uint32_t win_base, uint32_t heavy_min,
-                                                  uint32_t huge_min, SegLists L, const uint32_t* skip) {
+                                                  uint32_t huge_min, SegLists L, const uint32_t* skip,
+                                                  const uint32_t* mdev = nullptr) {
     if (skip && *skip) return;   // k_sort_local built the lists
+    if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path)
     __shared__ uint32_t s_k[SEG_TILE + SEG_TILE / 16];
     __shared__ uint32_t s_next[256];      // first head of chunk t, then of chunks > t
     __shared__ uint32_t s_cnt[4], s_base[4], s_open, s_open_end;
@@ -1033,7 +1035,8 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
                                                  const CfgDev* __restrict__ cfgs, int32_t profile,
                                                  const ReqRec<XS>* __restrict__ rec, const int64_t* __restrict__ n_in,
-                                                 ReqArgs out, TbPre pre) {
+                                                 ReqArgs out, TbPre pre, const uint32_t* mdev = nullptr) {
+    if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < m; base += stride) {

@@ -67,6 +67,8 @@ __device__ inline uint32_t block_excl_scan_256(uint32_t v, uint32_t* s_tmp /*[4]
 // an atomic counter until every tile is done (a grid smaller than the tile
 // count is persistent; a tile only ever waits on tiles already taken).
 // skip (nullable): a device flag that turns the pass into a no-op.
+// mdev (nullable): the batch size in device memory, at most m (the grid is
+// sized for m; tiles past the device size exit at once).
 // plan (nullable, the MSD pass of the grouping sort): the block of tile 0
 // writes plan[0] = 1 when no digit of this pass holds more than plan_cap
 // elements (every bucket then fits k_sort_local) and plan[1] = 1 otherwise,
@@ -76,8 +78,9 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, uint32_t m, int shift, const uint32_t* __restrict__ ghist,
     uint32_t* status, uint32_t* tile_ctr, uint32_t* eflags, const uint32_t* skip = nullptr,
-    uint32_t* plan = nullptr, uint32_t plan_cap = 0, uint32_t* plan_host = nullptr) {
+    uint32_t* plan = nullptr, uint32_t plan_cap = 0, uint32_t* plan_host = nullptr, const uint32_t* mdev = nullptr) {
     if (skip && *skip) return;
+    if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path): m is its bound
     __shared__ uint32_t s_wcnt[SORT_WAVES][RADIX];
     __shared__ uint32_t s_goff[RADIX];
     __shared__ uint32_t s_tmp[SORT_WAVES];

@@ -196,11 +196,11 @@ _sig = {
     "rl_route_owner": (C.c_int, [vp, C.c_size_t, vp, vp, vp]),
     "rl_stream_create_dedicated": (C.c_int, [C.c_int32, C.POINTER(vp)]),
     "rl_stream_destroy": (C.c_int, [vp]),
+    "rl_router_capacity": (C.c_uint32, [vp]),
     "rl_route_pack": (C.c_int, [vp, C.c_size_t] + [vp] * 8),
-    "rl_route_merge": (C.c_int, [vp, C.c_size_t] + [vp] * 10),
-    "rl_route_results": (C.c_int, [C.c_size_t] + [vp] * 7),
-    "rl_route_unpack": (C.c_int, [C.c_size_t] + [vp] * 7),
-    "rl_route_results_local": (C.c_int, [C.c_size_t] + [vp] * 11),
+    "rl_route_merge": (C.c_int, [vp] + [vp] * 6),
+    "rl_route_unpack": (C.c_int, [vp, C.c_size_t] + [vp] * 7),
+    "rl_decide_routed_device": (C.c_int, [vp, C.c_size_t] + [vp] * 6),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -292,6 +292,13 @@ class Engine:
         out.status = rc
         return out
 
+    def decide_routed(self, m_max, count_p, recv_p, order_p, sms_p, res_p, stream=None):
+        """rl_decide_routed_device (include/rl_route.h): the merged routed
+        batch (its size in device memory at count_p, at most m_max)"""
+        rc = lib.rl_decide_routed_device(self.h, m_max, count_p, recv_p, order_p, sms_p, res_p, stream)
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+
     def decide_device(self, m, key_p, ts_p, n_p, cfg_p, sms_p, dec_p, rem_p, retry_p, reset_p, tok_p,
                       stream=None):
         rc = lib.rl_decide_batch_device(self.h, m, key_p, ts_p, n_p, cfg_p, sms_p, dec_p, rem_p,
@@ -376,18 +383,25 @@ def release_dedicated_streams():
         lib.rl_stream_destroy(_DEDICATED_STREAMS.pop())
 
 
+# rl_route.h
+RL_EOVERFLOW = -75
+DROPPED = 4
+
+
 class Router:
     """rl_router (include/rl_route.h): the routing kernels of one rank.  All
-    arguments are device pointers (ints) and a hipStream_t; asynchronous."""
+    arguments are device pointers (ints) and a hipStream_t; asynchronous.
+    `cap`: records per peer bucket (rounded up: self.capacity)."""
 
-    def __init__(self, device, world, max_batch, max_recv):
+    def __init__(self, device, world, max_batch, cap):
         h = vp()
-        rc = lib.rl_router_create(device, world, max_batch, max_recv, C.byref(h))
+        rc = lib.rl_router_create(device, world, max_batch, cap, C.byref(h))
         if rc != RL_OK:
             raise EngineError(rc, "rl_router_create failed")
         self.h = h
         self.world = world
         self.device = device
+        self.capacity = lib.rl_router_capacity(h)
 
     def _chk(self, rc, what):
         if rc != RL_OK:
@@ -410,28 +424,11 @@ class Router:
     def pack(self, m, key, ts, n, cfg, send, send_info, slot, stream):
         self._chk(lib.rl_route_pack(self.h, m, key, ts, n, cfg, send, send_info, slot, stream), "rl_route_pack")
 
-    def merge(self, m_recv, recv, recv_info, recv_info_host, key, ts, n, cfg, sms, at, stream):
-        self._chk(lib.rl_route_merge(self.h, m_recv, recv, recv_info, recv_info_host, key, ts, n, cfg, sms, at,
-                                     stream),
-                  "rl_route_merge")
+    def merge(self, recv, recv_info, order, sms, count, stream):
+        self._chk(lib.rl_route_merge(self.h, recv, recv_info, order, sms, count, stream), "rl_route_merge")
 
-    @staticmethod
-    def results(m_recv, at, dec, rem, retry, reset, res, stream):
-        rc = lib.rl_route_results(m_recv, at, dec, rem, retry, reset, res, stream)
-        if rc != RL_OK:
-            raise EngineError(rc, "rl_route_results")
-
-    @staticmethod
-    def unpack(m, slot, back, dec, rem, retry, reset, stream):
-        rc = lib.rl_route_unpack(m, slot, back, dec, rem, retry, reset, stream)
-        if rc != RL_OK:
-            raise EngineError(rc, "rl_route_unpack")
-
-    @staticmethod
-    def results_local(m, slot, at, dec_in, rem_in, retry_in, reset_in, dec, rem, retry, reset, stream):
-        rc = lib.rl_route_results_local(m, slot, at, dec_in, rem_in, retry_in, reset_in, dec, rem, retry, reset, stream)
-        if rc != RL_OK:
-            raise EngineError(rc, "rl_route_results_local")
+    def unpack(self, m, slot, back, dec, rem, retry, reset, stream):
+        self._chk(lib.rl_route_unpack(self.h, m, slot, back, dec, rem, retry, reset, stream), "rl_route_unpack")
 
     def sync(self, stream=None) -> int:
         return lib.rl_router_sync(self.h, stream)

@@ -7,39 +7,52 @@
  * store applies each key's requests in arrival order.  Here the key space is
  * split over the GPUs of a node -- GPU owner(k) = (mix64(k) >> 32) mod G keeps
  * key k's state in its HBM tables -- and every GPU accepts requests for any
- * key.  One step of G ranks, each with a batch of requests:
+ * key.  One step of G ranks, each with a batch of requests, runs with no host
+ * involvement at all (nothing is read back to size anything):
  *
  *   sender   rl_route_pack      owner of every request; requests grouped by
- *                               owner (stable) into 32-byte records; per owner
- *                               {count, the batch's earliest and latest ts,
- *                               whether the batch is in time order} (int64)
- *            all-to-all of the counts, then of the records (RCCL over xGMI;
- *            the caller drives the collectives, e.g. torch.distributed "nccl")
- *   owner    rl_route_merge     the received records -- grouped by source rank,
- *                               each group in its source's order -- in the
- *                               order ONE shared store sees them: by arrival
- *                               time, ties by (source rank, source position),
- *                               where a request arrives at the running max of
- *                               its source's ts so far (each source's own order
- *                               is kept, also for a batch out of time order);
- *                               written as the key/ts/n/cfg/server_ms arrays
- *                               rl_decide_batch_device takes
- *            rl_decide_batch_device (include/rl_engine.h) on them
- *            rl_route_results   results back to received order, 32-byte records
- *            all-to-all of the results (the counts reversed)
+ *                               owner (stable) into fixed-capacity buckets of
+ *                               `cap` 32-byte records, send[o * cap + j]; per
+ *                               owner an info row {count sent, earliest ts,
+ *                               latest ts, count dropped}.  A request past
+ *                               its owner's capacity is dropped: never
+ *                               executed, decision RL_DROPPED, and the
+ *                               router's sticky status reports RL_EOVERFLOW
+ *            equal-split all-to-alls of the info rows and of the buckets
+ *            (RCCL over xGMI; the caller drives the collectives, e.g.
+ *            torch.distributed "nccl"): every split is `cap` records, so the
+ *            collectives need no host-side sizes
+ *   owner    rl_route_merge     the received buckets -- source s's `count`
+ *                               records at recv[s * cap], in its order -- in
+ *                               the order ONE shared store sees them: by
+ *                               arrival time, ties by (source rank, source
+ *                               position), where a request arrives at the
+ *                               running max of its source's ts so far (each
+ *                               source's own order is kept, also for a batch
+ *                               out of time order).  Planned on the device:
+ *                               per-source running maxima, then a tree of
+ *                               merge-path merges; writes the decision order
+ *                               order[p] (a receive index), each request's
+ *                               store clock server_ms[p] and the number
+ *                               received into *count (device memory)
+ *            rl_decide_routed_device: the owner's engine reads the received
+ *                               records in that order and writes 32-byte
+ *                               result records at their receive index
+ *            equal-split all-to-all of the result buckets back
  *   sender   rl_route_unpack    results to the caller's order
  *
  * The store's clock (Redis TTLs) is one clock that never goes back: request
  * p of step b expires keys at server_ms = max(floor(arrival_p / 1e6), the
  * latest floor(ts / 1e6) of any request of any rank in steps before b).
- * Every owner learns each rank's latest ts through the count exchange, so all
- * owners keep the same clock, and per key the clock never decreases (merge
- * order is arrival order), which is what makes expiry exact (rl_window.h).
+ * Every owner learns each rank's latest ts through the info rows, so all
+ * owners keep the same clock (in device memory), and per key the clock never
+ * decreases (merge order is arrival order), which is what makes expiry exact
+ * (rl_window.h).
  *
  * Every array is device memory; every call is asynchronous on `stream` (a
- * hipStream_t).  Requirement: the timestamps one owner receives in a step
- * span less than 2^48 ns (78 hours); a violation is reported by
- * rl_router_sync (RL_EINVAL) and the merge order is then unspecified.
+ * hipStream_t).  Calls on one router use its scratch: packs must run in step
+ * order, merges too (the store clock), e.g. each on one stream or ordered by
+ * events.
  */
 #ifndef RL_ROUTE_H
 #define RL_ROUTE_H
@@ -53,7 +66,11 @@
 extern "C" {
 #endif
 
-/* one routed request (send and receive buffers) */
+#define RL_EOVERFLOW (-75)     /* a request exceeded its owner's bucket capacity (rl_router_sync) */
+#define RL_DROPPED 4           /* decision: not executed, its owner's bucket was full (resubmit it) */
+#define RL_ROUTE_INFO 4        /* int64 per info row: count sent, earliest ts, latest ts, count dropped */
+
+/* one routed request (send and receive buckets) */
 typedef struct rl_route_rec {
     uint64_t key;
     int64_t ts;
@@ -72,11 +89,16 @@ typedef struct rl_route_res {
 
 typedef struct rl_router rl_router;
 
-/* scratch for batches of up to max_batch sent and max_recv received requests */
-int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t max_recv, rl_router** out);
+/* scratch for batches of up to max_batch requests and buckets of `cap`
+ * records per peer (rounded up to a multiple of 2048; rl_router_capacity).
+ * cap = max_batch can never drop a request; a hash partition of a uniform
+ * key stream needs about max_batch / world plus a margin. */
+int rl_router_create(int32_t device, int32_t world, uint32_t max_batch, uint32_t cap, rl_router** out);
 int rl_router_destroy(rl_router* r);
+/* the bucket capacity in records (every split of the collectives) */
+uint32_t rl_router_capacity(const rl_router* r);
 /* wait for the router's queued work on `stream`; returns and clears the
- * sticky status (RL_EINVAL: ts span >= 2^48 ns, RL_ETIMEOUT: sort look-back) */
+ * sticky status: RL_EOVERFLOW when a request was dropped since the last sync */
 int rl_router_sync(rl_router* r, void* stream);
 
 /* A stream on a hardware queue of its own (CU-masked with every CU, which
@@ -90,50 +112,33 @@ int rl_stream_destroy(void* stream);
 /* owner of each key id (the partition: (mix64(k) >> 32) mod world) */
 int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner, void* stream);
 
-/* sender: requests grouped by owner -> send[m] (owner 0's first, each group in
- * batch order); send_info[RL_ROUTE_INFO * o + k]: k = 0 requests for owner o,
- * 1 the batch's earliest ts, 2 its latest ts (INT64_MAX / INT64_MIN if empty),
- * 3 nonzero when the batch's ts never decrease -- RL_ROUTE_INFO int64 per
- * owner, exchanged with an equal-split all-to-all; slot[i] = request i's
- * position in send (for rl_route_unpack) */
-#define RL_ROUTE_INFO 4
+/* sender: request i for owner o is the j-th of the batch's requests for o
+ * (batch order); j < cap: send[o * cap + j], slot[i] = o * cap + j; else
+ * dropped, slot[i] = UINT32_MAX.  send_info[RL_ROUTE_INFO * o + k]: k = 0
+ * requests sent to o (<= cap), 1 the batch's earliest ts, 2 its latest ts
+ * (INT64_MAX / INT64_MIN if the batch is empty), 3 requests for o dropped. */
 int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
                   const uint32_t* cfg, rl_route_rec* send, int64_t* send_info, uint32_t* slot, void* stream);
 
-/* owner: recv[m_recv] (grouped by source rank) -> the decision order; writes
- * key/ts/n/cfg/server_ms[m_recv] for rl_decide_batch_device and at[i] = the
- * position of received record i in that order.  recv_info: the received
- * send_info rows (source r's at [RL_ROUTE_INFO * r]) in device memory, and
- * recv_info_host: the same rows on the host (the caller read them to size the
- * record exchange).  The merge is planned on the host from them: when only
- * one source sent records, the received order already is the decision order
- * and the merge is one gather kernel (when every source's batch is in time
- * order, arrival = ts and no running max is taken); otherwise only the sort
- * passes the step's time span needs are launched.  The rows also advance the
- * store clock after this step.  Call once per step, in step order, also when
- * m_recv is 0.  recv_info_host NULL (world 1 only: one source): the merge is
- * planned on the device -- no host read of the rows, the store clock kept in
- * device memory from then on (a router then takes no host-planned merge:
- * RL_EINVAL) -- as a per-tile max, one scan block and one gather. */
-int rl_route_merge(rl_router* r, size_t m_recv, const rl_route_rec* recv, const int64_t* recv_info,
-                   const int64_t* recv_info_host, uint64_t* key, int64_t* ts, int64_t* n, uint32_t* cfg,
-                   int64_t* server_ms, uint32_t* at, void* stream);
+/* owner: recv[world * cap] (source s's bucket at s * cap) and recv_info (the
+ * received info rows, source s's at RL_ROUTE_INFO * s) -> the decision order:
+ * order[p] = receive index of the p-th request, server_ms[p] its store clock,
+ * *count = requests received (p < *count are valid).  Call once per step, in
+ * step order (it advances the store clock). */
+int rl_route_merge(rl_router* r, const rl_route_rec* recv, const int64_t* recv_info, uint32_t* order,
+                   int64_t* server_ms, uint32_t* count, void* stream);
 
-/* owner: decisions (in the merge order) -> res[i] for received record i */
-int rl_route_results(size_t m_recv, const uint32_t* at, const uint8_t* decision, const int64_t* remaining,
-                     const int64_t* retry_after_ns, const int64_t* reset_at_ns, rl_route_res* res, void* stream);
+/* owner: the engine on the merged requests -- request p is recv[order[p]]
+ * with store clock server_ms[p], p < *count (device memory, at most m_max <=
+ * the engine's max_batch); its result goes to res[order[p]].  The grouping
+ * waits for `stream` (the merge); `stream` waits for the results. */
+int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
+                            const uint32_t* order, const int64_t* server_ms, rl_route_res* res, void* stream);
 
-/* sender: back[m] (send layout) -> the caller's order */
-int rl_route_unpack(size_t m, const uint32_t* slot, const rl_route_res* back, uint8_t* decision,
+/* sender: back[world * cap] (the result buckets, send layout) -> the caller's
+ * order; a dropped request gets decision RL_DROPPED and zeros */
+int rl_route_unpack(rl_router* r, size_t m, const uint32_t* slot, const rl_route_res* back, uint8_t* decision,
                     int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns, void* stream);
-
-/* one GPU (nothing exchanged between the two): rl_route_results and
- * rl_route_unpack in one pass -- the caller's outputs for request i from the
- * engine's outputs at position at[slot[i]] */
-int rl_route_results_local(size_t m, const uint32_t* slot, const uint32_t* at, const uint8_t* decision_in,
-                           const int64_t* remaining_in, const int64_t* retry_in, const int64_t* reset_in,
-                           uint8_t* decision, int64_t* remaining, int64_t* retry_after_ns, int64_t* reset_at_ns,
-                           void* stream);
 
 #ifdef __cplusplus
 }

@@ -26,98 +26,97 @@ def running_max_by_source(ts, src):
     return out
 
 
+CAP_ALIGN = 2048      # rl_route.hip: bucket capacities are multiples of the merge tile
+DROPPED_SLOT = -1     # slot of a dropped request (UINT32_MAX as int32)
+
+
 class NumpyRouteOps:
-    def __init__(self, world):
+    """the routing kernels of include/rl_route.h on host pointers"""
+
+    def __init__(self, world, cap):
         self.world = world
+        self.capacity = (cap + CAP_ALIGN - 1) // CAP_ALIGN * CAP_ALIGN
         self.clock = -(1 << 63)     # the store clock of the next step (ms)
+        self.overflow = False
 
     def pack(self, m, key, ts, n, cfg, send, scnt, slot, stream):
+        cap = self.capacity
         k = _arr(key, m, np.int64).view(np.uint64)
         own = shard.owner_of(k, self.world)
-        order = np.argsort(own, kind="stable")
-        snd = _arr(send, 4 * m, np.int64).reshape(m, 4)
+        snd = _arr(send, 4 * self.world * cap, np.int64).reshape(self.world * cap, 4)
         c = _arr(cfg, m, np.int32).view(np.uint32).astype(np.int64)
         rec = np.stack([k.view(np.int64), _arr(ts, m, np.int64), _arr(n, m, np.int64),
                         c | (np.arange(m, dtype=np.int64) << 32)], 1)
-        snd[:] = rec[order]
         info = _arr(scnt, 4 * self.world, np.int64).reshape(self.world, 4)
         t = _arr(ts, m, np.int64)
-        info[:, 0] = np.bincount(own, minlength=self.world)
-        info[:, 1] = t.min() if m else (1 << 63) - 1
-        info[:, 2] = t.max() if m else -(1 << 63)
-        info[:, 3] = int(bool(np.all(t[1:] >= t[:-1])))
         sl = _arr(slot, m, np.int32)
-        sl[order] = np.arange(m, dtype=np.int32)
+        for o in range(self.world):
+            idx = np.nonzero(own == o)[0]          # batch order
+            keep = idx[:cap]
+            snd[o * cap:o * cap + keep.size] = rec[keep]
+            sl[keep] = o * cap + np.arange(keep.size, dtype=np.int32)
+            sl[idx[cap:]] = DROPPED_SLOT
+            self.overflow |= idx.size > cap
+            info[o] = [keep.size, t.min() if m else (1 << 63) - 1, t.max() if m else -(1 << 63), idx.size - keep.size]
 
-    def merge(self, m, recv, info, info_host, key, ts, n, cfg, sms, at, stream):
-        latest = _arr(info, 4 * self.world, np.int64).reshape(self.world, 4)[:, 2]
+    def merge(self, recv, info, order, sms, count, stream):
+        cap, G = self.capacity, self.world
+        rows = _arr(info, 4 * G, np.int64).reshape(G, 4)
         c0 = self.clock
-        live = latest[latest != -(1 << 63)]
-        if live.size:
-            self.clock = max(c0, int(live.max()) // 1_000_000)
-        if m == 0:
-            return
-        rec = _arr(recv, 4 * m, np.int64).reshape(m, 4)
-        rows = _arr(info, 4 * self.world, np.int64).reshape(self.world, 4)
-        sent = rows[:, 0] > 0
-        arrive = rec[:, 1].copy()
-        if not np.all(rows[sent, 3] != 0):
-            # a request arrives at the running max of its source's ts so far
-            src = np.minimum(np.searchsorted(np.cumsum(rows[:, 0]), np.arange(m), side="right"), self.world - 1)
-            arrive = running_max_by_source(rec[:, 1], src)
-        if np.count_nonzero(sent) <= 1:
-            o = np.arange(m)                            # one source: its own order
-        else:
-            o = np.argsort(arrive, kind="stable")       # arrival order, ties by received order
-        _arr(key, m, np.int64)[:] = rec[o, 0]
-        _arr(ts, m, np.int64)[:] = rec[o, 1]
-        _arr(n, m, np.int64)[:] = rec[o, 2]
-        _arr(cfg, m, np.int32)[:] = (rec[o, 3] & 0xffffffff).astype(np.uint32).view(np.int32)
-        _arr(sms, m, np.int64)[:] = np.maximum(arrive[o] // 1_000_000, c0)
-        a = _arr(at, m, np.int32)
-        a[o] = np.arange(m, dtype=np.int32)
+        latest = rows[:, 2][rows[:, 2] != -(1 << 63)]
+        if latest.size:
+            self.clock = max(c0, int(latest.max()) // 1_000_000)
+        rec = _arr(recv, 4 * G * cap, np.int64).reshape(G * cap, 4)
+        cnt = np.clip(rows[:, 0], 0, cap)
+        arrive, src, pos = [], [], []
+        for s in range(G):
+            a = np.maximum.accumulate(rec[s * cap:s * cap + cnt[s], 1]) if cnt[s] else np.zeros(0, np.int64)
+            arrive.append(a)
+            src.append(np.full(cnt[s], s))
+            pos.append(np.arange(cnt[s]))
+        arrive, src, pos = (np.concatenate(x) if x else np.zeros(0, np.int64) for x in (arrive, src, pos))
+        o = np.lexsort((pos, src, arrive))          # arrival, ties by (source rank, source position)
+        tot = int(cnt.sum())
+        _arr(order, max(tot, 1), np.int32)[:tot] = (src[o] * cap + pos[o]).astype(np.int32)
+        _arr(sms, max(tot, 1), np.int64)[:tot] = np.maximum(arrive[o] // 1_000_000, c0)
+        _arr(count, 1, np.int32)[0] = tot
 
-    @staticmethod
-    def results(m, at, dec, rem, retry, reset, res, stream):
-        a = _arr(at, m, np.int32)
-        r = _arr(res, 4 * m, np.int64).reshape(m, 4)
-        r[:, 0] = _arr(dec, m, np.uint8)[a]
-        r[:, 1] = _arr(rem, m, np.int64)[a]
-        r[:, 2] = _arr(retry, m, np.int64)[a]
-        r[:, 3] = _arr(reset, m, np.int64)[a]
-
-    @staticmethod
-    def unpack(m, slot, back, dec, rem, retry, reset, stream):
+    def unpack(self, m, slot, back, dec, rem, retry, reset, stream):
         s = _arr(slot, m, np.int32)
-        b = _arr(back, 4 * m, np.int64).reshape(m, 4)[s]
-        _arr(dec, m, np.uint8)[:] = b[:, 0]
-        _arr(rem, m, np.int64)[:] = b[:, 1]
-        _arr(retry, m, np.int64)[:] = b[:, 2]
-        _arr(reset, m, np.int64)[:] = b[:, 3]
+        b = _arr(back, 4 * self.world * self.capacity, np.int64).reshape(self.world * self.capacity, 4)
+        dropped = s == DROPPED_SLOT
+        r = b[np.where(dropped, 0, s).astype(np.int64)]
+        r[dropped] = [4, 0, 0, 0]                   # RL_DROPPED
+        _arr(dec, m, np.uint8)[:] = r[:, 0]
+        _arr(rem, m, np.int64)[:] = r[:, 1]
+        _arr(retry, m, np.int64)[:] = r[:, 2]
+        _arr(reset, m, np.int64)[:] = r[:, 3]
 
 
-def oracle_decide(sim):
-    """engine decide() over host pointers, backed by the CPU oracle"""
-    def decide(m, key, ts, n, cfg, sms, dec, rem, retry, reset, stream):
-        if m == 0:
+def oracle_decide(sim, world, cap):
+    """the owner's engine (rl_decide_routed_device) over host pointers,
+    backed by the CPU oracle: request p is recv[order[p]], p < count"""
+    def decide(m_max, count, recv, order, sms, res, stream):
+        cnt = int(_arr(count, 1, np.int32)[0])
+        if cnt == 0:
             return
-        d, r, rt, rs, _ = sim.decide(_arr(key, m, np.int64).view(np.uint64), _arr(ts, m, np.int64),
-                                     _arr(n, m, np.int64), _arr(cfg, m, np.int32).view(np.uint32),
-                                     _arr(sms, m, np.int64))
-        _arr(dec, m, np.uint8)[:] = d
-        _arr(rem, m, np.int64)[:] = r
-        _arr(retry, m, np.int64)[:] = rt
-        _arr(reset, m, np.int64)[:] = rs
+        o = _arr(order, cnt, np.int32).astype(np.int64)
+        rec = _arr(recv, 4 * world * cap, np.int64).reshape(world * cap, 4)[o]
+        d, r, rt, rs, _ = sim.decide(rec[:, 0].view(np.uint64), rec[:, 1], rec[:, 2],
+                                     (rec[:, 3] & 0xffffffff).astype(np.uint32), _arr(sms, cnt, np.int64))
+        out = _arr(res, 4 * world * cap, np.int64).reshape(world * cap, 4)
+        out[o] = np.stack([d.astype(np.int64), r, rt, rs], 1)
     return decide
 
 
-def shared_limiter_expectations(all_batches, rank, configs, profile=0):
+def shared_limiter_expectations(all_batches, rank, configs, profile=0, cap=None):
     """decisions of ONE shared limiter over every rank's batches, step by step,
     each step in (arrival, source rank, source position) order -- a request's
     arrival is the running max of ts over the requests its rank sent to the
     same owner so far -- with the store's clock max(floor(arrival / 1e6), the
     latest ts of earlier steps) (include/rl_route.h); per step, `rank`'s
-    results in its batch order"""
+    results in its batch order.  cap: a rank's requests for one owner past the
+    first `cap` of the step are dropped (never reach the store, RL_DROPPED)."""
     import oracle
     ref = oracle.OracleSim(profile)
     for a, L, W in configs:
@@ -132,19 +131,25 @@ def shared_limiter_expectations(all_batches, rank, configs, profile=0):
         pos = np.concatenate([np.arange(p[0].size) for p in parts])
         own = shard.owner_of(U[0].astype(np.uint64), world)
         arrive = np.empty_like(U[1])
+        sent = np.ones(U[0].size, bool)
         for r in range(world):
             for w in range(world):
                 idx = np.nonzero((src == r) & (own == w))[0]
+                if cap is not None and idx.size > cap:
+                    sent[idx[cap:]] = False
+                    idx = idx[:cap]
                 if idx.size:
                     arrive[idx] = np.maximum.accumulate(U[1][idx])
-        o = np.lexsort((pos, src, arrive))
+        live = np.nonzero(sent)[0]
+        o = live[np.lexsort((pos[live], src[live], arrive[live]))]
         sms = np.maximum(arrive[o] // 1_000_000, clock)
         if U[1].size:
             clock = max(clock, int(U[1].max()) // 1_000_000)
         d, rm, rt, rs, _ = ref.decide(U[0][o], U[1][o], U[2][o], U[3][o], sms)
-        mine = src[o] == rank
-        exp_pos = pos[o][mine]
-        inv = np.empty_like(exp_pos)
-        inv[exp_pos] = np.arange(exp_pos.size)
-        outs.append([x[mine][inv] for x in (d, rm, rt, rs)])
+        full = [np.zeros(U[0].size, np.int64) for _ in range(4)]
+        full[0][:] = 4                             # RL_DROPPED unless decided
+        for f, x in enumerate((d, rm, rt, rs)):
+            full[f][o] = x
+        mine = src == rank
+        outs.append([x[mine] for x in full])
     return outs

@@ -32,7 +32,7 @@ def test_headers_declare_the_boundary():
     for must in ["rl_engine_create", "rl_engine_destroy", "rl_config_register", "rl_decide_batch",
                  "rl_decide_batch_device", "rl_reset", "rl_last_error", "rll_new", "rll_allow_n",
                  "rl_coalescer_create", "rl_coalescer_submit", "rl_coalescer_wait", "rl_route_pack",
-                 "rl_route_merge", "rl_route_results", "rl_route_unpack"]:
+                 "rl_route_merge", "rl_decide_routed_device", "rl_route_unpack"]:
         assert must in names
 
 

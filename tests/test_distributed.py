@@ -52,7 +52,7 @@ def skewed_rank_batches(rank, nbatch=4, m=3000, nkeys=200):
     return out
 
 
-def _pipeline_worker(rank, world, port, q):
+def _pipeline_worker(rank, world, port, q, m=3000, cap=4096, exchange=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "distributed-rate-limiter_amd", "python"),
@@ -70,44 +70,58 @@ def _pipeline_worker(rank, world, port, q):
         for a, L, W in CONFIGS:
             sim.add_config(a, L, W)
         pg_res = dist.new_group(backend="gloo")
-        pipe = shard.RoutedPipeline(route_ops.NumpyRouteOps(world), route_ops.oracle_decide(sim), world, 4000,
-                                    "cpu", pg_req=None, pg_res=pg_res, depth=4, lookahead=2)
-        all_batches = [skewed_rank_batches(r) for r in range(world)]
+        ops = route_ops.NumpyRouteOps(world, cap)
+        pipe = shard.RoutedPipeline(ops, route_ops.oracle_decide(sim, world, ops.capacity), world, m, "cpu",
+                                    pg_req=None, pg_res=pg_res, depth=4, exchange=exchange)
+        all_batches = [skewed_rank_batches(r, m=m) for r in range(world)]
         mine = all_batches[rank]
         ins = [tuple(torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else
                                       (x.view(np.int32) if x.dtype == np.uint32 else x)) for x in bt) for bt in mine]
         outs = [(torch.empty(b[0].size, dtype=torch.uint8),) + tuple(torch.empty(b[0].size, dtype=torch.int64)
                                                                    for _ in range(3)) for b in mine]
         pipe.run(ins, outs)
-        exp = route_ops.shared_limiter_expectations(all_batches, rank, CONFIGS)
+        exp = route_ops.shared_limiter_expectations(all_batches, rank, CONFIGS, cap=ops.capacity)
         ok = all(np.array_equal(o.numpy().astype(np.int64), np.asarray(e, np.int64))
                  for ob, eb in zip(outs, exp) for o, e in zip(ob, eb))
-        q.put((rank, ok))
+        # 3 collectives per step (info rows, records, results), nothing sized on the host
+        ok = ok and pipe.exchange and pipe.collectives == 3 * len(mine) and pipe.wait_s == 0.0
+        q.put((rank, ok, ops.overflow))
     finally:
         dist.destroy_process_group()
 
 
-def test_routed_pipeline_matches_single_shared_limiter():
-    """shard.RoutedPipeline (lookahead count exchange, two process groups,
-    rotating buffer sets) over world size 2 on CPU, with the kernels' CPU
-    restatement and the oracle as the owner's engine: every rank's results
-    equal one shared limiter over the union of the ranks' requests."""
+def _run_ranks(world, **kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipeline_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_pipeline_worker, args=(r, world, port, q), kwargs=kw) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = {r: (ok, ov) for r, ok, ov in (q.get(timeout=300) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
-    assert res == {0: True, 1: True}
+    return res
+
+
+def test_routed_pipeline_matches_single_shared_limiter():
+    """shard.RoutedPipeline (fixed-capacity buckets, equal-split all-to-alls,
+    two process groups, rotating buffer sets, no host read) over world size 2
+    on CPU, with the kernels' CPU restatement and the oracle as the owner's
+    engine: every rank's results equal one shared limiter over the union of
+    the ranks' requests."""
+    assert _run_ranks(2) == {0: (True, False), 1: (True, False)}
+
+
+def test_routed_pipeline_bucket_overflow_drops_requests():
+    """buckets smaller than a rank's requests for one owner: the requests past
+    the capacity are dropped at the sender (RL_DROPPED, never applied) and
+    every other decision still equals the shared limiter without them"""
+    assert _run_ranks(2, m=5000, cap=2048) == {0: (True, True), 1: (True, True)}
 
 
 def test_routed_pipeline_world1_local_mode():
-    """world size 1: the pipeline runs no collective and reads nothing back
-    (records and results read in place, merge planned without host rows);
-    the results still equal the one shared limiter, batches out of time order
+    """world size 1: no collective (buckets and results read in place); the
+    results still equal the one shared limiter, batches out of time order
     included (CPU restatement of the kernels, oracle as the engine)"""
     import torch
 
@@ -117,16 +131,23 @@ def test_routed_pipeline_world1_local_mode():
     sim = oracle.OracleSim(0)
     for a, L, W in CONFIGS:
         sim.add_config(a, L, W)
-    pipe = shard.RoutedPipeline(route_ops.NumpyRouteOps(1), route_ops.oracle_decide(sim), 1, 4000, "cpu",
-                                depth=4, lookahead=2)
-    assert pipe.local
+    ops = route_ops.NumpyRouteOps(1, 4000)
+    pipe = shard.RoutedPipeline(ops, route_ops.oracle_decide(sim, 1, ops.capacity), 1, 4000, "cpu", depth=4)
+    assert not pipe.exchange
     mine = skewed_rank_batches(1)
     ins = [tuple(torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else
                                   (x.view(np.int32) if x.dtype == np.uint32 else x)) for x in bt) for bt in mine]
     outs = [(torch.empty(b[0].size, dtype=torch.uint8),) + tuple(torch.empty(b[0].size, dtype=torch.int64)
                                                                for _ in range(3)) for b in mine]
     pipe.run(ins, outs)
+    assert pipe.collectives == 0
     exp = route_ops.shared_limiter_expectations([mine], 0, CONFIGS)
     for ob, eb in zip(outs, exp):
         for o, e in zip(ob, eb):
             assert np.array_equal(o.numpy().astype(np.int64), np.asarray(e, np.int64))
+
+
+def test_routed_pipeline_world1_exchange_over_gloo():
+    """world size 1 with the exchange forced on: the loopback all-to-alls run
+    (a one-rank gloo group) and change nothing"""
+    assert _run_ranks(1, exchange=True) == {0: (True, False)}

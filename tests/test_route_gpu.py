@@ -26,11 +26,20 @@ def _dev_tensors(torch, *arrays):
     return out
 
 
-@pytest.mark.parametrize("world", [1, 2, 3, 8])
-def test_route_kernels_match_restatement(rl, world):
+def _host(torch, *arrays):
+    return [torch.from_numpy(np.ascontiguousarray(x.view(np.int64) if x.dtype == np.uint64 else
+                                                  (x.view(np.int32) if x.dtype == np.uint32 else x)))
+            for x in arrays]
+
+
+@pytest.mark.parametrize("world,cap", [(1, 70_001), (2, 40_000), (3, 20_000), (8, 9_000), (8, 4096), (2, 30_000)])
+def test_route_pack_matches_restatement(rl, world, cap):
+    """owner buckets, info rows and slots; the last three cases overflow
+    their buckets (dropped requests: slot UINT32_MAX, RL_EOVERFLOW)"""
     import torch
 
     import route_ops
+    import shard
     rng = np.random.default_rng(40 + world)
     m = 70_001
     key = rng.integers(0, 1 << 63, m).astype(np.uint64)
@@ -38,9 +47,12 @@ def test_route_kernels_match_restatement(rl, world):
     ts[rng.random(m) < 0.2] = T0 + 12345                              # many equal times
     n = rng.integers(1, 9, m).astype(np.int64)
     cfg = rng.integers(0, 15, m).astype(np.uint32)
-    r = rl.Router(0, world, m, m)
+    r = rl.Router(0, world, m, cap)
+    ops = route_ops.NumpyRouteOps(world, cap)
+    assert r.capacity == ops.capacity and r.capacity % 2048 == 0
+    C = r.capacity
     k, t, nn, c = _dev_tensors(torch, key, ts, n, cfg)
-    send = torch.empty((m, 4), dtype=torch.int64, device="cuda")
+    send = torch.empty((world * C, 4), dtype=torch.int64, device="cuda")
     scnt = torch.empty((world, 4), dtype=torch.int64, device="cuda")
     slot = torch.empty(m, dtype=torch.int32, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
@@ -48,173 +60,105 @@ def test_route_kernels_match_restatement(rl, world):
            slot.data_ptr(), s)
     own = torch.empty(m, dtype=torch.int32, device="cuda")
     r.owner(m, k.data_ptr(), own.data_ptr(), s)
-    # CPU restatement
-    ops = route_ops.NumpyRouteOps(world)
-    kc, tc, nc, cc = [torch.from_numpy(np.ascontiguousarray(x.view(np.int64) if x.dtype == np.uint64 else
-                                                            (x.view(np.int32) if x.dtype == np.uint32 else x)))
-                      for x in (key, ts, n, cfg)]
-    send_h = torch.empty((m, 4), dtype=torch.int64)
+    kc, tc, nc, cc = _host(torch, key, ts, n, cfg)
+    send_h = torch.zeros((world * C, 4), dtype=torch.int64)
     scnt_h = torch.empty((world, 4), dtype=torch.int64)
     slot_h = torch.empty(m, dtype=torch.int32)
     ops.pack(m, kc.data_ptr(), tc.data_ptr(), nc.data_ptr(), cc.data_ptr(), send_h.data_ptr(), scnt_h.data_ptr(),
              slot_h.data_ptr(), None)
     torch.cuda.synchronize()
-    import shard
     assert np.array_equal(own.cpu().numpy(), shard.owner_of(key, world))
-    assert torch.equal(scnt.cpu(), scnt_h) and torch.equal(send.cpu(), send_h) and torch.equal(slot.cpu(), slot_h)
-    # merge of the packed records (as if received), twice: the second step
-    # starts from the store clock the first one left
-    info = torch.tensor([[m // world, int(ts.min()), int(ts.max()) + r * 100_000_000, 0] for r in range(world)],
-                        dtype=torch.int64)
-    for step in range(2):
-        outs = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
-               [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
-                torch.empty(m, dtype=torch.int32, device="cuda")]
-        info_d = info.cuda()
-        r.merge(m, send.data_ptr(), info_d.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs], s)
-        outs_h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
-                 [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
-        ops.merge(m, send_h.data_ptr(), info.data_ptr(), info.data_ptr(), *[x.data_ptr() for x in outs_h], None)
-        assert r.sync(s) == rl.RL_OK
-        for a, b in zip(outs, outs_h):
-            assert torch.equal(a.cpu(), b)
-    # results + unpack
-    dec = torch.from_numpy(rng.integers(0, 4, m).astype(np.uint8))
-    rem, retry, reset = [torch.from_numpy(rng.integers(-5, 1 << 40, m).astype(np.int64)) for _ in range(3)]
-    res = torch.empty((m, 4), dtype=torch.int64, device="cuda")
-    dd = [x.cuda() for x in (dec, rem, retry, reset)]
-    r.results(m, outs[5].data_ptr(), *[x.data_ptr() for x in dd], res.data_ptr(), s)
-    res_h = torch.empty((m, 4), dtype=torch.int64)
-    ops.results(m, outs_h[5].data_ptr(), *[x.data_ptr() for x in (dec, rem, retry, reset)], res_h.data_ptr(), None)
-    back = [torch.empty(m, dtype=torch.uint8, device="cuda")] + [torch.empty(m, dtype=torch.int64, device="cuda")
-                                                                 for _ in range(3)]
-    r.unpack(m, slot.data_ptr(), res.data_ptr(), *[x.data_ptr() for x in back], s)
-    back_h = [torch.empty(m, dtype=torch.uint8)] + [torch.empty(m, dtype=torch.int64) for _ in range(3)]
-    ops.unpack(m, slot_h.data_ptr(), res_h.data_ptr(), *[x.data_ptr() for x in back_h], None)
-    torch.cuda.synchronize()
-    assert torch.equal(res.cpu(), res_h)
-    for a, b in zip(back, back_h):
-        assert torch.equal(a.cpu(), b)
+    assert torch.equal(scnt.cpu(), scnt_h) and torch.equal(slot.cpu(), slot_h)
+    sd = send.cpu()
+    for o in range(world):
+        c_o = int(scnt_h[o, 0])
+        assert torch.equal(sd[o * C:o * C + c_o], send_h[o * C:o * C + c_o])
+    dropped = int(scnt_h[:, 3].sum())
+    assert (dropped > 0) == ops.overflow
+    assert r.sync(s) == (rl.RL_EOVERFLOW if dropped else rl.RL_OK)
+    assert r.sync(s) == rl.RL_OK        # sticky until read, then cleared
     r.close()
 
 
-def test_merge_single_sorted_source_keeps_order(rl):
-    """one source whose batch is in time order: no sort, the received order
-    is the decision order (and the store clock still advances)"""
+def _merge_case(rng, world, C, counts, span, step_base):
+    """received buckets: source q's counts[q] records, times unsorted within
+    a source, with ties across sources"""
+    recv = np.zeros((world * C, 4), np.int64)
+    info = np.zeros((world, 4), np.int64)
+    for q in range(world):
+        c = counts[q]
+        ts = step_base + rng.integers(0, span, c).astype(np.int64)
+        ts[rng.random(c) < 0.1] = step_base + 777_000                   # ties across sources
+        recv[q * C:q * C + c] = np.stack([rng.integers(0, 1 << 62, c), ts, rng.integers(1, 4, c),
+                                          np.arange(c, dtype=np.int64) << 32], 1)
+        info[q] = [c, ts.min() if c else (1 << 63) - 1, ts.max() if c else -(1 << 63), 0]
+    return recv, info
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_route_merge_matches_restatement(rl, world):
+    """the device-planned merge over three steps (the store clock carried in
+    device memory; step 3's times go back below it): decision order, store
+    clocks and received count against the restatement; empty and full
+    buckets, sources out of time order, equal times across sources"""
     import torch
 
     import route_ops
-    m = 9000
-    rng = np.random.default_rng(4)
-    ts = T0 + np.cumsum(rng.integers(0, 5000, m)).astype(np.int64)
-    rec = np.stack([rng.integers(0, 1 << 62, m), ts, np.ones(m, np.int64), np.arange(m, dtype=np.int64) << 32], 1)
-    info = np.array([[m, ts.min(), ts.max(), 1]], np.int64)
-    r = rl.Router(0, 1, m, m)
-    ops = route_ops.NumpyRouteOps(1)
+    rng = np.random.default_rng(17 + world)
+    cap = 9000
+    r = rl.Router(0, world, 4096, cap)
+    ops = route_ops.NumpyRouteOps(world, cap)
+    C = r.capacity
     s = torch.cuda.current_stream().cuda_stream
-    for step in range(2):
-        d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
-            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
-             torch.empty(m, dtype=torch.int32, device="cuda")]
-        h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
-            [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
-        rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
-        r.merge(m, rt.data_ptr(), it.data_ptr(), torch.from_numpy(info).data_ptr(), *[x.data_ptr() for x in d], s)
-        rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
-        ops.merge(m, rh.data_ptr(), ih.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
-        assert r.sync(s) == rl.RL_OK
-        for a, b in zip(d, h):
-            assert torch.equal(a.cpu(), b)
-        assert np.array_equal(d[5].cpu().numpy(), np.arange(m))
-    r.close()
-
-
-def test_merge_planned_on_the_device_one_source(rl):
-    """world 1 without host rows (rl_route_merge(..., NULL, ...)): per-tile
-    maxima, one scan block that advances the store clock in device memory, one
-    gather -- the same outputs as the restatement over three steps, batches
-    out of time order and one step whose times go back below the clock; a
-    host-planned merge on that router is then refused"""
-    import torch
-
-    import route_ops
-    m = 25_000
-    rng = np.random.default_rng(17)
-    r = rl.Router(0, 1, m, m)
-    ops = route_ops.NumpyRouteOps(1)
-    s = torch.cuda.current_stream().cuda_stream
-    base = [T0, T0 + 4_000_000_000, T0 + 1_000_000_000]      # step 3 goes back in time
+    base = [T0, T0 + 4_000_000_000, T0 + 1_000_000_000]
     for step in range(3):
-        ts = base[step] + rng.integers(0, 3_000_000_000, m).astype(np.int64)   # unsorted, 3 s span
-        rec = np.stack([rng.integers(0, 1 << 62, m), ts, rng.integers(1, 4, m), np.arange(m, dtype=np.int64) << 32],
-                       1)
-        info = np.array([[m, ts.min(), ts.max(), 0]], np.int64)
-        d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
-            [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
-             torch.empty(m, dtype=torch.int32, device="cuda")]
-        h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
-            [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
-        rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
-        r.merge(m, rt.data_ptr(), it.data_ptr(), None, *[x.data_ptr() for x in d], s)
-        rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
-        ops.merge(m, rh.data_ptr(), ih.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
+        counts = rng.integers(0, C + 1, world)
+        counts[rng.integers(world)] = C if world > 1 else counts[0]
+        if world > 2:
+            counts[rng.integers(world)] = 0
+        recv, info = _merge_case(rng, world, C, counts, 3_000_000_000, base[step])
+        rt, it = torch.from_numpy(recv).cuda(), torch.from_numpy(info).cuda()
+        order = torch.full((world * C,), -7, dtype=torch.int32, device="cuda")
+        sms = torch.empty(world * C, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        r.merge(rt.data_ptr(), it.data_ptr(), order.data_ptr(), sms.data_ptr(), cnt.data_ptr(), s)
+        rh, ih = torch.from_numpy(recv), torch.from_numpy(info)
+        order_h = torch.empty(world * C, dtype=torch.int32)
+        sms_h = torch.empty(world * C, dtype=torch.int64)
+        cnt_h = torch.zeros(1, dtype=torch.int32)
+        ops.merge(rh.data_ptr(), ih.data_ptr(), order_h.data_ptr(), sms_h.data_ptr(), cnt_h.data_ptr(), None)
         assert r.sync(s) == rl.RL_OK
-        for a, b in zip(d, h):
-            assert torch.equal(a.cpu(), b)
-    with pytest.raises(rl.EngineError):
-        r.merge(m, rt.data_ptr(), it.data_ptr(), torch.from_numpy(info).data_ptr(), *[x.data_ptr() for x in d], s)
+        tot = int(counts.sum())
+        assert int(cnt.cpu()[0]) == int(cnt_h[0]) == tot
+        assert torch.equal(order.cpu()[:tot], order_h[:tot])
+        assert torch.equal(sms.cpu()[:tot], sms_h[:tot])
     r.close()
 
 
-@pytest.mark.parametrize("span_bits", [33, 41])
-def test_merge_wide_time_spans_and_unsorted_sources(rl, span_bits):
-    """received times spanning more than 2^32 ns (five and six sort passes),
-    three sources out of time order: arrival order against the restatement"""
+def test_route_unpack_dropped_and_kept(rl):
     import torch
 
     import route_ops
-    world = 3
-    m = 30_000
-    rng = np.random.default_rng(span_bits)
-    ts = T0 + rng.integers(0, 1 << span_bits, m).astype(np.int64)
-    rec = np.stack([rng.integers(0, 1 << 62, m), ts, np.ones(m, np.int64), np.arange(m, dtype=np.int64) << 32], 1)
-    cnt = [10_000, 12_000, 8_000]
-    info = np.array([[c, T0, T0 + (1 << span_bits), 0] for c in cnt], np.int64)
-    info[:, 1] = [ts[:10_000].min(), ts[10_000:22_000].min(), ts[22_000:].min()]
-    info[:, 2] = [ts[:10_000].max(), ts[10_000:22_000].max(), ts[22_000:].max()]
-    r = rl.Router(0, world, m, m)
-    ops = route_ops.NumpyRouteOps(world)
-    s = torch.cuda.current_stream().cuda_stream
-    d = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
-        [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
-         torch.empty(m, dtype=torch.int32, device="cuda")]
-    h = [torch.empty(m, dtype=torch.int64) for _ in range(3)] + \
-        [torch.empty(m, dtype=torch.int32), torch.empty(m, dtype=torch.int64), torch.empty(m, dtype=torch.int32)]
-    rt, it = torch.from_numpy(rec).cuda(), torch.from_numpy(info).cuda()
-    r.merge(m, rt.data_ptr(), it.data_ptr(), torch.from_numpy(info).data_ptr(), *[x.data_ptr() for x in d], s)
-    rh, ih = torch.from_numpy(rec), torch.from_numpy(info)
-    ops.merge(m, rh.data_ptr(), ih.data_ptr(), ih.data_ptr(), *[x.data_ptr() for x in h], None)
-    assert r.sync(s) == rl.RL_OK
-    for a, b in zip(d, h):
+    rng = np.random.default_rng(5)
+    world, m, cap = 3, 20_000, 4096
+    r = rl.Router(0, world, m, cap)
+    C = r.capacity
+    slot = rng.integers(0, world * C, m).astype(np.int32)
+    slot[rng.random(m) < 0.1] = -1
+    back = rng.integers(-5, 1 << 40, (world * C, 4)).astype(np.int64)
+    back[:, 0] = rng.integers(0, 4, world * C)
+    st, bt = torch.from_numpy(slot).cuda(), torch.from_numpy(back).cuda()
+    outs = [torch.empty(m, dtype=torch.uint8, device="cuda")] + [torch.empty(m, dtype=torch.int64, device="cuda")
+                                                                 for _ in range(3)]
+    r.unpack(m, st.data_ptr(), bt.data_ptr(), *[x.data_ptr() for x in outs], torch.cuda.current_stream().cuda_stream)
+    ops = route_ops.NumpyRouteOps(world, cap)
+    outs_h = [torch.empty(m, dtype=torch.uint8)] + [torch.empty(m, dtype=torch.int64) for _ in range(3)]
+    sh, bh = torch.from_numpy(slot), torch.from_numpy(back)
+    ops.unpack(m, sh.data_ptr(), bh.data_ptr(), *[x.data_ptr() for x in outs_h], None)
+    torch.cuda.synchronize()
+    for a, b in zip(outs, outs_h):
         assert torch.equal(a.cpu(), b)
-    r.close()
-
-
-def test_merge_reports_a_too_wide_time_span(rl):
-    import torch
-    m = 5000
-    r = rl.Router(0, 2, m, m)
-    rec = torch.zeros((m, 4), dtype=torch.int64, device="cuda")
-    rec[:, 1] = T0
-    rec[7, 1] = T0 + (1 << 49)
-    outs = [torch.empty(m, dtype=torch.int64, device="cuda") for _ in range(3)] + \
-           [torch.empty(m, dtype=torch.int32, device="cuda"), torch.empty(m, dtype=torch.int64, device="cuda"),
-            torch.empty(m, dtype=torch.int32, device="cuda")]
-    s = torch.cuda.current_stream().cuda_stream
-    info_h = torch.tensor([[m - 100, T0, T0 + (1 << 49), 0], [100, T0, T0, 1]], dtype=torch.int64)
-    info = info_h.cuda()
-    r.merge(m, rec.data_ptr(), info.data_ptr(), info_h.data_ptr(), *[x.data_ptr() for x in outs], s)
-    assert r.sync(s) == rl.RL_EINVAL
+    assert int((outs_h[0] == rl.DROPPED).sum()) >= int((slot == -1).sum())
     r.close()
 
 
@@ -226,10 +170,11 @@ def _free_port():
     return p
 
 
-def _routed_rank(rank, world, port, backend, batches_of, q):
+def _routed_rank(rank, world, port, backend, batches_of, q, exchange=None, cap=None):
     """one rank of the native routed path on cuda:0: Router kernels, the HIP
-    engine as owner, all-to-alls over `backend` (nccl: RCCL; gloo: through
-    host memory, for two ranks sharing the box's one GPU)"""
+    engine as owner (rl_decide_routed_device), equal-split all-to-alls over
+    `backend` (nccl: RCCL; gloo: through host memory, for two ranks sharing
+    the box's one GPU)"""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "distributed-rate-limiter_amd", "python"), os.path.join(root, "tests")]
@@ -243,21 +188,19 @@ def _routed_rank(rank, world, port, backend, batches_of, q):
     torch.cuda.set_device(0)
     dist.init_process_group(backend, rank=rank, world_size=world)
     ok = False
+    info = {}
     try:
         all_batches = [batches_of(r) for r in range(world)]
         mine = all_batches[rank]
         mb = max(b[0].size for b in mine)
-        eng = rl_amd.Engine(profile=0, tb_capacity=1 << 20, win_capacity=1 << 20, max_batch=world * mb)
+        router = rl_amd.Router(0, world, mb, cap or mb)
+        eng = rl_amd.Engine(profile=0, tb_capacity=1 << 20, win_capacity=1 << 20,
+                            max_batch=world * router.capacity)
         for a, L, W in CONFIGS:
             eng.register(a, L, W)
-
-        def decide(m, key, ts, n, cfg, sms, dec, rem, retry, reset, stream):
-            eng.decide_device(m, key, ts, n, cfg, sms, dec, rem, retry, reset, None, stream)
-
-        router = rl_amd.Router(0, world, mb, world * mb)
         pg_res = dist.new_group(backend=backend)
-        pipe = shard.RoutedPipeline(router, decide, world, mb, "cuda:0", pg_req=None, pg_res=pg_res,
-                                    staged=backend == "gloo")
+        pipe = shard.RoutedPipeline(router, eng.decide_routed, world, mb, "cuda:0", pg_req=None, pg_res=pg_res,
+                                    exchange=exchange, staged=backend == "gloo")
         ins = [tuple(_dev_tensors(torch, *bt)) for bt in mine]
         outs = [(torch.empty(b[0].size, dtype=torch.uint8, device="cuda"),) +
                 tuple(torch.empty(b[0].size, dtype=torch.int64, device="cuda") for _ in range(3)) for b in mine]
@@ -265,8 +208,10 @@ def _routed_rank(rank, world, port, backend, batches_of, q):
         pipe.run(ins, outs)
         torch.cuda.synchronize()
         assert eng.sync() == rl_amd.RL_OK, eng.last_error()
-        assert router.sync(None) == rl_amd.RL_OK
-        exp = route_ops.shared_limiter_expectations(all_batches, rank, CONFIGS)
+        info["router_status"] = router.sync(None)
+        info["collectives"] = pipe.collectives
+        info["exchange"] = pipe.exchange
+        exp = route_ops.shared_limiter_expectations(all_batches, rank, CONFIGS, cap=router.capacity)
         ok = True
         for b, (ob, eb) in enumerate(zip(outs, exp)):
             for f, (o, e) in enumerate(zip(ob, eb)):
@@ -276,10 +221,12 @@ def _routed_rank(rank, world, port, backend, batches_of, q):
                     ok = False
                     print(f"rank {rank} batch {b} field {f}: {bad.size} mismatches, first {bad[:5]} "
                           f"got {g[bad[:5]]} exp {e[bad[:5]]} keys {mine[b][0][bad[:5]]}", flush=True)
+        info["dropped"] = int(sum((o[0].cpu().numpy() == rl_amd.DROPPED).sum() for o in outs))
+        del pipe
         eng.close()
         router.close()
     finally:
-        q.put((rank, ok))
+        q.put((rank, ok, info))
         dist.destroy_process_group()
 
 
@@ -300,36 +247,63 @@ def mixed_batches(rank, nbatch=4, m=150_000, nkeys=300_000):
     return out
 
 
-def _spawn(world, backend, batches_of):
+def _spawn(world, backend, batches_of, **kw):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_routed_rank, args=(r, world, port, backend, batches_of, q)) for r in range(world)]
+    procs = [ctx.Process(target=_routed_rank, args=(r, world, port, backend, batches_of, q), kwargs=kw)
+             for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in procs)
+    res = {r: (ok, info) for r, ok, info in (q.get(timeout=240) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
     return res
 
 
+def _check(res, world, nbatch, exchange, dropped=False):
+    for r in range(world):
+        ok, info = res[r]
+        assert ok, (r, info)
+        assert info["exchange"] == exchange
+        # three equal-split collectives per step (info rows, request buckets,
+        # result buckets), or none at all
+        assert info["collectives"] == (3 * nbatch if exchange else 0), info
+        assert (info["dropped"] > 0) == dropped
+        assert info["router_status"] == (-75 if dropped else 0), info
+
+
 def test_routed_path_one_rank_rccl():
-    """world size 1 over RCCL: the full native routed path (pack, count and
-    record all-to-alls, time-order merge, engine, result all-to-all, unpack)"""
-    assert _spawn(1, "nccl", mixed_batches) == {0: True}
+    """world size 1 with the exchange forced on: the full native routed path
+    over RCCL -- pack, loopback all-to-alls of the info rows and of the
+    request buckets, device-planned merge, the engine on the received records,
+    result all-to-all, unpack -- with device tensors"""
+    _check(_spawn(1, "nccl", mixed_batches, exchange=True), 1, 4, True)
+
+
+def test_routed_path_one_rank_local():
+    """world size 1 without the exchange: buckets and results read in place"""
+    _check(_spawn(1, "nccl", mixed_batches), 1, 4, False)
 
 
 def test_routed_path_two_ranks_one_gpu():
     """two ranks (two engines, two routers) on the box's one GPU; the
     all-to-alls go through host memory (gloo), the kernels are the GPU's"""
-    assert _spawn(2, "gloo", mixed_batches) == {0: True, 1: True}
+    _check(_spawn(2, "gloo", mixed_batches), 2, 4, True)
+
+
+def test_routed_path_two_ranks_bucket_overflow():
+    """buckets smaller than a rank's requests for one owner: the requests past
+    the capacity come back RL_DROPPED, were never applied, and every other
+    decision equals the shared limiter without them; the router reports
+    RL_EOVERFLOW"""
+    _check(_spawn(2, "gloo", mixed_batches, cap=60_000), 2, 4, True, dropped=True)
 
 
 def skewed_batches(rank, nbatch=3, m=60_000, nkeys=20_000):
     """app servers with skewed clocks (tracegen.skewed_trace): every batch out
-    of time order, spans of minutes (five sort passes), per-key time going
-    back by windows"""
+    of time order, spans of minutes, per-key time going back by windows"""
     import tracegen
     k, ts, n, cfg, _ = tracegen.skewed_trace(900 + rank, nbatch * m, nkeys, CONFIGS)
     return [(k[b * m:(b + 1) * m], ts[b * m:(b + 1) * m], n[b * m:(b + 1) * m], cfg[b * m:(b + 1) * m])
@@ -337,11 +311,12 @@ def skewed_batches(rank, nbatch=3, m=60_000, nkeys=20_000):
 
 
 def test_routed_path_one_rank_unsorted_batches():
-    """world size 1 with batches out of time order: the routed path applies a
-    rank's requests in its own order (as rl_decide_batch_device does), with
-    the store clock at each request's arrival (the running max of ts)"""
-    assert _spawn(1, "nccl", skewed_batches) == {0: True}
+    """world size 1 over RCCL (exchange forced on) with batches out of time
+    order: the routed path applies a rank's requests in its own order (as
+    rl_decide_batch_device does), with the store clock at each request's
+    arrival (the running max of ts)"""
+    _check(_spawn(1, "nccl", skewed_batches, exchange=True), 1, 3, True)
 
 
 def test_routed_path_two_ranks_unsorted_batches():
-    assert _spawn(2, "gloo", skewed_batches) == {0: True, 1: True}
+    _check(_spawn(2, "gloo", skewed_batches), 2, 3, True)
