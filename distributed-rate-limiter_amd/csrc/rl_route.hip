@@ -66,9 +66,11 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_owner(uint32_t m, const uint
 __device__ inline unsigned long long bias(int64_t t) { return (unsigned long long)t ^ 0x8000000000000000ull; }
 __device__ inline int64_t unbias(unsigned long long u) { return (int64_t)(u ^ 0x8000000000000000ull); }
 
-// summary of a batch (pack): earliest / latest ts (biased)
+// summary of a batch (pack): earliest / latest ts (biased), whether ts ever
+// decreases (a source in time order needs no running max at its owners)
 struct PackSum {
     unsigned long long lo, hi;
+    uint32_t unsorted;
 };
 
 
@@ -79,18 +81,26 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint6
                                                          uint32_t* __restrict__ tile_cnt, PackSum* tile_sum) {
     __shared__ uint32_t s_cnt[MAX_WORLD];
     __shared__ unsigned long long s_lo[RT_BLOCK / 64], s_hi[RT_BLOCK / 64];
+    __shared__ uint32_t s_uns;
     if (threadIdx.x < MAX_WORLD) s_cnt[threadIdx.x] = 0;
+    if (threadIdx.x == 0) s_uns = 0;
     __syncthreads();
     const uint32_t base = blockIdx.x * RT_TILE;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     unsigned long long lo = ~0ull, hi = 0;
+    uint32_t uns = 0;
 #pragma unroll
     for (int j = 0; j < RT_ITEMS; j++) {
         const uint32_t i = base + j * RT_BLOCK + threadIdx.x;
         const bool ok = i < m;
         const uint32_t own = ok ? owner_of(key[i], world) : 0u;
         const int64_t t = ok ? ts[i] : 0;
+        // a wave's 64 requests are consecutive: the predecessor's ts is the
+        // lane below (lane 0 loads it)
+        int64_t tp = __shfl_up(t, 1);
+        if (lane == 0) tp = (ok && i > 0) ? ts[i - 1] : t;
+        if (ok && i > 0 && tp > t) uns = 1;
         // one LDS add per owner per wave (not per request: at small world
         // every request of a tile would hit one counter)
         const uint64_t peers = owner_peers(own, world, ok);
@@ -110,9 +120,10 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_hist(uint32_t m, const uint6
         s_lo[threadIdx.x >> 6] = lo;
         s_hi[threadIdx.x >> 6] = hi;
     }
+    if (uns) s_uns = 1;   // benign race: every writer stores 1
     __syncthreads();
     if (threadIdx.x == 0) {
-        PackSum t{~0ull, 0ull};
+        PackSum t{~0ull, 0ull, s_uns};
         for (int w = 0; w < RT_BLOCK / 64; w++) {
             t.lo = s_lo[w] < t.lo ? s_lo[w] : t.lo;
             t.hi = s_hi[w] > t.hi ? s_hi[w] : t.hi;
@@ -133,14 +144,20 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scan(uint32_t tiles, uint32_
                                                          int64_t* __restrict__ info) {
     __shared__ uint32_t s_tmp[RT_BLOCK / 64];
     __shared__ unsigned long long s_lo[RT_BLOCK / 64], s_hi[RT_BLOCK / 64];
+    __shared__ uint32_t s_uns;
     const uint32_t o = blockIdx.x, tid = threadIdx.x;
+    if (tid == 0) s_uns = 0;
+    __syncthreads();
     // the batch summary from the tiles' summaries
     unsigned long long lo = ~0ull, hi = 0;
+    uint32_t uns = 0;
     for (uint32_t t = tid; t < tiles; t += RT_BLOCK) {
         const PackSum ps = tile_sum[t];
         lo = ps.lo < lo ? ps.lo : lo;
         hi = ps.hi > hi ? ps.hi : hi;
+        uns |= ps.unsorted;
     }
+    if (uns) s_uns = 1;
     for (int off = 32; off > 0; off >>= 1) {
         const unsigned long long l2 = __shfl_xor(lo, off), h2 = __shfl_xor(hi, off);
         lo = l2 < lo ? l2 : lo;
@@ -175,7 +192,8 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_scan(uint32_t tiles, uint32_
         row[0] = run < cap ? run : cap;
         row[1] = tiles ? unbias(lo) : INT64_MAX;
         row[2] = tiles ? unbias(hi) : INT64_MIN;
-        row[3] = run > cap ? run - cap : 0;
+        // dropped requests, and bit 0: the batch's ts decrease somewhere
+        row[3] = (int64_t)(run > cap ? run - cap : 0) * 2 + (s_uns ? 1 : 0);
     }
 }
 
@@ -264,6 +282,10 @@ __device__ inline uint32_t recv_count(const int64_t* __restrict__ info, uint32_t
     const int64_t c = info[(size_t)RL_ROUTE_INFO * s];
     return c <= 0 ? 0u : (c >= (int64_t)cap ? cap : (uint32_t)c);
 }
+// the source's batch never goes back in time: arrival = ts, no running max
+__device__ inline bool recv_sorted(const int64_t* __restrict__ info, uint32_t s) {
+    return (info[(size_t)RL_ROUTE_INFO * s + 3] & 1) == 0;
+}
 
 // per tile of MT_TILE received records: the max biased ts (scan inputs).
 // Tile t is source t / tps's tile t % tps.
@@ -273,6 +295,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_bm_tmax(const rl_route_rec* __rest
     __shared__ unsigned long long s_w[RT_BLOCK / 64];
     const uint32_t s = blockIdx.x / tps, u = blockIdx.x % tps;
     const uint32_t c = recv_count(info, s, cap);
+    if (recv_sorted(info, s)) return;   // block-uniform: no scan inputs needed
     unsigned long long mx = 0;
     if (u * MT_TILE < c) {
 #pragma unroll
@@ -306,7 +329,7 @@ __global__ __launch_bounds__(1024) void k_bm_tscan(const int64_t* __restrict__ i
     __shared__ unsigned long long s_carry;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t s = blockIdx.x;
-    const uint32_t tiles = (recv_count(info, s, cap) + MT_TILE - 1) / MT_TILE;
+    const uint32_t tiles = recv_sorted(info, s) ? 0u : (recv_count(info, s, cap) + MT_TILE - 1) / MT_TILE;
     unsigned long long* t_s = tmax + (size_t)s * tps;
     if (tid == 0) s_carry = 0;
     __syncthreads();
@@ -364,6 +387,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_bm_keys(const rl_route_rec* __rest
     if (u * MT_TILE >= c) return;   // block-uniform
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t i0 = u * MT_TILE + threadIdx.x * MT_ITEMS;
+    const bool sorted = recv_sorted(info, s);    // block-uniform
     unsigned long long a[MT_ITEMS];
     unsigned long long run = 0;
 #pragma unroll
@@ -371,19 +395,22 @@ __global__ __launch_bounds__(RT_BLOCK) void k_bm_keys(const rl_route_rec* __rest
         const uint32_t i = i0 + q;
         a[q] = i < c ? (unsigned long long)rec[(size_t)s * cap + i].ts ^ TS_BIAS : 0ull;
         run = a[q] > run ? a[q] : run;
-        a[q] = run;                                  // inclusive within the thread
+        if (!sorted) a[q] = run;                 // inclusive within the thread
     }
-    unsigned long long inc = run;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long v = __shfl_up(inc, o, 64);
-        if (lane >= (uint32_t)o) inc = v > inc ? v : inc;
+    unsigned long long ex = 0;
+    if (!sorted) {
+        unsigned long long inc = run;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long v = __shfl_up(inc, o, 64);
+            if (lane >= (uint32_t)o) inc = v > inc ? v : inc;
+        }
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        unsigned long long pre = tpre[blockIdx.x];
+        for (uint32_t k = 0; k < w; k++) pre = s_w[k] > pre ? s_w[k] : pre;
+        ex = __shfl_up(inc, 1, 64);
+        ex = lane ? (ex > pre ? ex : pre) : pre;
     }
-    if (lane == 63) s_w[w] = inc;
-    __syncthreads();
-    unsigned long long pre = tpre[blockIdx.x];
-    for (uint32_t k = 0; k < w; k++) pre = s_w[k] > pre ? s_w[k] : pre;
-    unsigned long long ex = __shfl_up(inc, 1, 64);
-    ex = lane ? (ex > pre ? ex : pre) : pre;
     const int64_t c0 = ctl->clock_prev;
 #pragma unroll
     for (int q = 0; q < MT_ITEMS; q++) {

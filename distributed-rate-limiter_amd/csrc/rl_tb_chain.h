@@ -855,11 +855,73 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
     }
 }
 
-// Exact serial steps by one wave (every lane computes the same values, lane 0
-// writes): from the exact stored state (D, E) before position q, the step at
-// q when `force` (a step that leaves the regime), then on while the state is
-// off the fast decades or the last step left the regime -- at most
-// CH_SERIAL steps and never at or past lim.  add_at(p): TbPre::add of p.
+// One Redis-7 script step in decimal mode on the stored state as doubles:
+// digits Dd (an integer-valued double, |Dd| in [1e13, 1e14), or 0) at scale
+// P = 10^(13 - E), k = 13 - E in [1, 22].  The common serial step -- the key
+// alive, the sum below th (no allow, no clamp) -- with %.14g's decade chosen
+// on the exact scaled value (as dec14_fast: a >= 10^E and a < 10^(E+1) tested
+// on a*P = p + err exactly; digits RNE, a carry to 1e14 moves up a decade) at
+// the same, the next or the one after next decade.  False when the step needs
+// the general path (tb_eval): sum >= th, or a decade outside k in [1, 22] or
+// more than two away.  Sign-symmetric like %.14g and strtod.  The same
+// arithmetic as tb_eval(QM_DEC) + its decade search, in about 25 dependent
+// double operations instead of the general path's integer conversions,
+// table lookups and branches.
+__device__ __attribute__((always_inline)) inline bool tb_dec_step(double& Dd, int32_t& E, double& P, double add,
+                                                                 double th, double& tokens) {
+    const double T = Dd / P;                     // strtod: one correctly rounded division (Clinger)
+    const double sum = T + add;
+    if (!(sum < th)) return false;               // allow or clamp: n and the capacity decide
+    tokens = sum;
+    const double a = sum < 0.0 ? -sum : sum;
+    if (a == 0.0) {                              // tostring(0) == "0": T = 0 at any scale
+        Dd = 0.0;
+        return true;
+    }
+    double Pn = P;
+    int32_t En = E;
+#pragma unroll
+    for (int g = 0; g < 3; g++) {
+        const double p = a * Pn, err = __builtin_fma(a, Pn, -p);    // a*Pn == p + err exactly
+        const bool lo_ok = (p > 1e13) | ((p == 1e13) & (err >= 0.0));
+        const bool hi_ok = (p < 1e14) | ((p == 1e14) & (err < 0.0));
+        if (lo_ok & hi_ok) {
+            double d = rint(p);                  // RNE of p; the exact product decides a tie of p
+            const double h = p - d;
+            d += ((h == 0.5) & (err > 0.0)) ? 1.0 : 0.0;
+            d -= ((h == -0.5) & (err < 0.0)) ? 1.0 : 0.0;
+            if (d == 1e14) {                     // rounding carried into the next decade
+                d = 1e13;
+                En += 1;
+                Pn = Pn / 10.0;                  // exact: a smaller power of ten
+            }
+            if (En > 12 || En < -9) return false;
+            Dd = sum < 0.0 ? -d : d;
+            E = En;
+            P = Pn;
+            return true;
+        }
+        if (!lo_ok) {
+            En -= 1;
+            Pn = Pn * 10.0;
+        } else {
+            En += 1;
+            Pn = Pn / 10.0;
+        }
+        if (En > 12 || En < -9) return false;    // 13 - E outside [1, 22]
+    }
+    return false;
+}
+
+// Exact serial steps by one wave (every lane computes the same values): from
+// the exact stored state (D, E) before position q, the step at q when `force`
+// (a step that leaves the regime), then on while the state is off the fast
+// decades or the last step left the regime -- at most CH_SERIAL steps and
+// never at or past lim.  add_at(p): TbPre::add of p.  Step k's outputs are
+// collected in lane k % 64 and stored 64 positions at a time (coalesced),
+// not one lane-0 store per step.  Redis 7 steps in decimal mode take
+// tb_dec_step; the rest (allows, clamps, expired keys, far decade jumps, the
+// binary profile) the general tb_eval.
 struct SerialOut {
     uint32_t q;        // next position
     int64_t D;         // exact stored state before it
@@ -884,6 +946,10 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     int32_t emode = fast_mode(D < 0 ? -D : D, E, profile);
     double Ps = 1.0, Rs = 1.0;
     if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
+    // the state as a double too (Dd == D while both are live; tb_dec_step
+    // updates Dd alone and D follows when the general path needs it)
+    double Dd = (double)D;
+    bool d_stale = false;
     // add and th = min(capacity, n) of the next 64 positions in one vector load
     // each (lane k holds position q + k; the chain's are in its LDS ring): a
     // step costs its arithmetic, not a dependent memory round trip.  n and the
@@ -891,24 +957,49 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     // the key has expired: below th the step denies without clamping whatever
     // they are, so only those steps load them (from HBM)
     double avec = 0.0, tvec = 0.0;
+    double otok = 0.0;
+    uint32_t odec = 0;
+    uint32_t g0 = q;       // first position of the outputs collected in the lanes
     uint32_t k = 0;
     for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
-        if ((k & 63u) == 0) {
+        const uint32_t kl = k & 63u;
+        if (kl == 0) {
+            if (k) {   // the previous 64 outputs
+                a.tok[g0 + lane] = otok;
+                a.dec[g0 + lane] = (uint8_t)odec;
+            }
+            g0 = q;
             const uint32_t pq = q + lane;
             avec = pq < lim ? add_at(pq) : 0.0;
             tvec = pq < lim ? th_at(pq) : 0.0;
         }
-        const uint32_t kl = k & 63u;
         const double add = __longlong_as_double(readlane_i64(__double_as_longlong(avec), kl));
         const bool alive = add == add;
         const double th = __longlong_as_double(readlane_i64(__double_as_longlong(tvec), kl));
+        if (profile == PROFILE_REDIS7 && emode == QM_DEC && alive) {
+            double tk;
+            if (tb_dec_step(Dd, E, Ps, add, th, tk)) {
+                otok = lane == kl ? tk : otok;
+                odec = lane == kl ? (uint32_t)DEC_DENIED : odec;
+                d_stale = true;
+                force = false;
+                mode = (Dd >= 1e13) ? QM_DEC : QM_NONE;   // E stays in the fast range
+                q++;
+                continue;
+            }
+        }
+        if (d_stale) {
+            D = (int64_t)Dd;
+            d_stale = false;
+        }
         TbEval v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, th, th, profile);
         if (!alive || v.clamped) {      // sum >= th or an expired key: the real n and capacity
             const int64_t nn = a.n[q];
             const double cap = cfgs[a.cfg[q]].limit_d;
             v = tb_eval(emode, D, E, Ps, Rs, alive, alive ? add : 0.0, cap, (double)nn, profile);
         }
-        if (lane == 0) write_out_tb(a, q, v.allowed ? DEC_ALLOWED : DEC_DENIED, v.tokens);
+        otok = lane == kl ? v.tokens : otok;
+        odec = lane == kl ? (uint32_t)(v.allowed ? DEC_ALLOWED : DEC_DENIED) : odec;
         force = v.allowed || v.clamped || !alive;
         const bool same = emode != QM_NONE && v.inrange;
         if (same) {
@@ -945,8 +1036,14 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
                 if (emode != QM_NONE) mode_scale(emode, E, Ps, Rs);
             }
         }
+        Dd = (double)D;
         mode = fast_mode(D, E, profile);
         q++;
+    }
+    if (d_stale) D = (int64_t)Dd;
+    if (k && lane < q - g0) {   // the last (partial) group of outputs
+        a.tok[g0 + lane] = otok;
+        a.dec[g0 + lane] = (uint8_t)odec;
     }
     return SerialOut{q, D, E, mode, k};
 }

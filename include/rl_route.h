@@ -14,7 +14,8 @@
  *                               owner (stable) into fixed-capacity buckets of
  *                               `cap` 32-byte records, send[o * cap + j]; per
  *                               owner an info row {count sent, earliest ts,
- *                               latest ts, count dropped}.  A request past
+ *                               latest ts, flags: 2 * count dropped + 1 if
+ *                               the batch's ts ever decrease}.  A request past
  *                               its owner's capacity is dropped: never
  *                               executed, decision RL_DROPPED, and the
  *                               router's sticky status reports RL_EOVERFLOW
@@ -68,7 +69,7 @@ extern "C" {
 
 #define RL_EOVERFLOW (-75)     /* a request exceeded its owner's bucket capacity (rl_router_sync) */
 #define RL_DROPPED 4           /* decision: not executed, its owner's bucket was full (resubmit it) */
-#define RL_ROUTE_INFO 4        /* int64 per info row: count sent, earliest ts, latest ts, count dropped */
+#define RL_ROUTE_INFO 4        /* int64 per info row: count sent, earliest ts, latest ts, 2 * dropped + unsorted */
 
 /* one routed request (send and receive buckets) */
 typedef struct rl_route_rec {
@@ -116,7 +117,9 @@ int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner,
  * (batch order); j < cap: send[o * cap + j], slot[i] = o * cap + j; else
  * dropped, slot[i] = UINT32_MAX.  send_info[RL_ROUTE_INFO * o + k]: k = 0
  * requests sent to o (<= cap), 1 the batch's earliest ts, 2 its latest ts
- * (INT64_MAX / INT64_MIN if the batch is empty), 3 requests for o dropped. */
+ * (INT64_MAX / INT64_MIN if the batch is empty), 3 twice the requests for o
+ * dropped, plus 1 when the batch's ts decrease somewhere (a source in time
+ * order needs no running max of its arrival times at the owner). */
 int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
                   const uint32_t* cfg, rl_route_rec* send, int64_t* send_info, uint32_t* slot, void* stream);
 

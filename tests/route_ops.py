@@ -57,7 +57,9 @@ class NumpyRouteOps:
             sl[keep] = o * cap + np.arange(keep.size, dtype=np.int32)
             sl[idx[cap:]] = DROPPED_SLOT
             self.overflow |= idx.size > cap
-            info[o] = [keep.size, t.min() if m else (1 << 63) - 1, t.max() if m else -(1 << 63), idx.size - keep.size]
+            unsorted = int(m > 1 and bool(np.any(t[1:] < t[:-1])))
+            info[o] = [keep.size, t.min() if m else (1 << 63) - 1, t.max() if m else -(1 << 63),
+                       2 * (idx.size - keep.size) + unsorted]
 
     def merge(self, recv, info, order, sms, count, stream):
         cap, G = self.capacity, self.world

@@ -81,8 +81,9 @@ def test_route_pack_matches_restatement(rl, world, cap):
 
 
 def _merge_case(rng, world, C, counts, span, step_base):
-    """received buckets: source q's counts[q] records, times unsorted within
-    a source, with ties across sources"""
+    """received buckets: source q's counts[q] records, times out of order in
+    the even sources (flagged in the info row) and sorted in the odd ones,
+    with ties across sources"""
     recv = np.zeros((world * C, 4), np.int64)
     info = np.zeros((world, 4), np.int64)
     for q in range(world):
@@ -91,7 +92,11 @@ def _merge_case(rng, world, C, counts, span, step_base):
         ts[rng.random(c) < 0.1] = step_base + 777_000                   # ties across sources
         recv[q * C:q * C + c] = np.stack([rng.integers(0, 1 << 62, c), ts, rng.integers(1, 4, c),
                                           np.arange(c, dtype=np.int64) << 32], 1)
-        info[q] = [c, ts.min() if c else (1 << 63) - 1, ts.max() if c else -(1 << 63), 0]
+        if q % 2 and c:                                                 # odd sources: in time order
+            ts = np.sort(ts)
+            recv[q * C:q * C + c, 1] = ts
+        unsorted = int(c > 1 and bool(np.any(ts[1:] < ts[:-1])))
+        info[q] = [c, ts.min() if c else (1 << 63) - 1, ts.max() if c else -(1 << 63), unsorted]
     return recv, info
 
 
