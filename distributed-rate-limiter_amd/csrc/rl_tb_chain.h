@@ -330,87 +330,6 @@ __device__ inline double tb_step_d(double Dpred, double P, double R, double add,
     return Dn;
 }
 
-// A near step's outcome as a function of its predecessor, from one exact
-// evaluation (decimal mode).  With T = strtod(D u) = RN(D / P) and
-// e(D) = T P - D (exact, |e| < u / 2, u = ulp(T) P), the step's stored digits
-// are D' = D + RNE(e(D) + c) where c = (RN(T + add) - T) P is the same for
-// every predecessor whose T and sum stay in T's binade (the sum rounds add to
-// T's grid, ties excepted).  Moving the predecessor by an integer d moves T by
-// q ulps, q = round((d - e) / u), and e to e' = e + q u - d: one fma and a
-// rint.  So after one exact evaluation at D1 (D0 = D1' - D1), the outcome at
-// D1 + d is D1 + d + D0 + (e' > thi) - (e' < tlo), thi / tlo the half-integer
-// thresholds of e + c around D0.  Any case the model does not cover exactly
-// (another binade, a sum at or above th, an e' within 2^-44 of a threshold, a
-// result near the decade's edges, a tie of the sum's rounding) falls back to
-// the full step.
-struct NearModel {
-    double pred1, T1, e1, g, u, uinv, dsum, D0, thi, tlo;
-    uint32_t exp;      // biased exponent of T1 (its binade)
-    bool valid;
-};
-
-__device__ inline uint32_t dexp(double x) {
-    return (uint32_t)((__builtin_bit_cast(uint64_t, x) >> 52) & 0x7ffu);
-}
-
-// the exact decimal step of tb_step_d<QM_DEC>, with its T and sum
-__device__ inline double tb_step_dec_ts(double Dpred, double P, double add, double th, double& T, double& sum) {
-    T = Dpred / P;
-    sum = T + add;
-    bool ge_lo;
-    double Dn = round_scaled_Pd(sum, P, ge_lo);
-    if (!(ge_lo & (Dn < (double)DEC_HI))) Dn = __builtin_nan("");
-    if (!(sum < th)) Dn = __builtin_nan("");
-    return Dn;
-}
-
-__device__ inline NearModel near_model(double pred1, double T1, double sum1, double Dn1, double P, double add) {
-    NearModel nm;
-    nm.pred1 = pred1;
-    nm.T1 = T1;
-    nm.exp = dexp(T1);
-    nm.e1 = __builtin_fma(T1, P, -pred1);                       // exact
-    nm.g = __builtin_bit_cast(double, (uint64_t)(nm.exp - 52u) << 52);   // ulp(T1) (T1 normal, >= 2^-970)
-    nm.u = nm.g * P;                                             // exact: a power of two times 10^k
-    nm.uinv = 1.0 / nm.u;
-    nm.dsum = sum1 - T1;                                         // exact (same binade)
-    const double rerr = nm.dsum - add;                           // the sum's rounding error, exact
-    const double hi = nm.dsum * P, lo = __builtin_fma(nm.dsum, P, -hi);   // c = hi + lo exactly
-    nm.D0 = Dn1 - pred1;
-    nm.thi = ((nm.D0 + 0.5) - hi) - lo;
-    nm.tlo = ((nm.D0 - 0.5) - hi) - lo;
-    nm.valid = (Dn1 == Dn1) && dexp(sum1) == nm.exp && nm.exp > 60u && fabs(rerr) != 0.5 * nm.g;
-    return nm;
-}
-
-// the outcome (stored digits) at predecessor pred from the model; false when
-// the model does not decide it exactly (the caller takes the full step)
-__device__ inline bool near_eval(const NearModel& nm, double pred, double th, double& Dn) {
-    const double d = pred - nm.pred1;                            // exact small integer
-    if (d == 0.0) {
-        Dn = nm.pred1 + nm.D0;
-        return true;
-    }
-    const double x = d - nm.e1;                                  // exact
-    double q = rint(x * nm.uinv);
-    double rem = __builtin_fma(-q, nm.u, x);                     // x - q u, exact
-    if (rem > 0.5 * nm.u) {
-        q += 1.0;
-        rem -= nm.u;
-    } else if (rem < -0.5 * nm.u) {
-        q -= 1.0;
-        rem += nm.u;
-    }
-    const double e = -rem;
-    const double Tc = __builtin_fma(q, nm.g, nm.T1);            // exact on T1's grid (same binade)
-    const double sc = Tc + nm.dsum;
-    const bool ok = dexp(Tc) == nm.exp && dexp(sc) == nm.exp && sc < th &&
-                    fabs(e - nm.thi) > 0x1p-44 && fabs(e - nm.tlo) > 0x1p-44;
-    const double adj = e > nm.thi ? 1.0 : (e < nm.tlo ? -1.0 : 0.0);
-    Dn = pred + nm.D0 + adj;
-    return ok && Dn >= (double)DEC_LO + 2.0 && Dn < (double)DEC_HI - 2.0;
-}
-
 __device__ inline int32_t fast_mode(int64_t D, int32_t E, int32_t profile) {
     if (profile == PROFILE_REDIS7)
         return (D >= DEC_LO && D < DEC_HI && 13 - E >= 1 && 13 - E <= 22) ? QM_DEC : QM_NONE;
@@ -814,27 +733,10 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
             const double r = rint(ad * P);
             int32_t est = 0, flip = 0;
             uint32_t stop_lane = 64;
-            // decimal mode: the first pass evaluates every near step exactly at
-            // its guessed predecessor and keeps a model of the step (NearModel);
-            // later passes evaluate the model at the re-guessed predecessor --
-            // an fma and a rint instead of a division and a %.14g rounding
-            NearModel nm;
-            nm.valid = false;
             for (int it = 0;; it++) {
+                double tk;
                 const double pred = pn + (double)(cbo + est);
-                double Dn;
-                bool cheap = false;
-                if (MODE == QM_DEC && it > 0 && nm.valid) cheap = near_eval(nm, pred, th, Dn);
-                if (!cheap) {
-                    if (MODE == QM_DEC) {
-                        double T, sm;
-                        Dn = tb_step_dec_ts(pred, P, ad, th, T, sm);
-                        if (it == 0 && v) nm = near_model(pred, T, sm, Dn, P, ad);
-                    } else {
-                        double tk;
-                        Dn = tb_step_d<MODE>(pred, P, R, ad, th, tk);
-                    }
-                }
+                const double Dn = tb_step_d<MODE>(pred, P, R, ad, th, tk);
                 const bool brk = v && !(Dn == Dn);
                 flip = (!v || brk) ? 0 : (int32_t)(Dn - (pred + r));
                 const int32_t incl = (int32_t)wave_scan_u32((uint32_t)flip, 0u,

@@ -73,7 +73,7 @@ def test_route_pack_matches_restatement(rl, world, cap):
     for o in range(world):
         c_o = int(scnt_h[o, 0])
         assert torch.equal(sd[o * C:o * C + c_o], send_h[o * C:o * C + c_o])
-    dropped = int((scnt_h[:, 3] >> 1).sum())          # row[3] = 2 * dropped + unsorted
+    dropped = int(scnt_h[:, 3].sum())
     assert (dropped > 0) == ops.overflow
     assert r.sync(s) == (rl.RL_EOVERFLOW if dropped else rl.RL_OK)
     assert r.sync(s) == rl.RL_OK        # sticky until read, then cleared
