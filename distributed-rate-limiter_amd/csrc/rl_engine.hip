@@ -196,7 +196,7 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             sk[i] = slot;
             // one record per request: k_permute's sorted-order gather then
             // touches one line fragment instead of four arrays
-            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r]);
+            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r], i);
             for (int p = 0; p < passes; p++)
                 atomicAdd(&lh[p][(slot >> ((shifts >> (8 * p)) & 31u)) & (RADIX - 1)], 1u);
         }
@@ -478,6 +478,7 @@ struct BatchSet {
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
     void* rec = nullptr;          // requests packed in arrival order (k_probe -> k_permute): ReqRec<XS>
+    void* recb = nullptr;         // ReqRec<false> in the MSD pass's bucket order (k_sort_pass -> k_permute)
     uint8_t* o_dec = nullptr;
     double* o_tok = nullptr;      // tokens (token bucket) / Remaining bits (window): finish_result
     // token-bucket precomputation (k_permute)
@@ -615,6 +616,7 @@ static void free_set(BatchSet& B) {
     for (auto* l : B.list) (void)hipFree(l);
     (void)hipFree(B.p_ts); (void)hipFree(B.p_n); (void)hipFree(B.p_sms); (void)hipFree(B.p_cfg);
     (void)hipFree(B.rec);
+    (void)hipFree(B.recb);
     (void)hipFree(B.o_dec);
     (void)hipFree(B.o_tok);
     (void)hipFree(B.q_add); (void)hipFree(B.q_th);
@@ -642,6 +644,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
     ok &= hipMalloc(&B.rec, sizeof(ReqRec<true>) * M) == hipSuccess;
+    ok &= hipMalloc(&B.recb, sizeof(ReqRec<false>) * M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
     ok &= hipMalloc(&B.o_tok, 8 * M) == hipSuccess;
     // q_add and q_th carry 128 elements of slack: the chain's loader wave
@@ -1013,10 +1016,14 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
+    // 16-byte records (no explicit server clock) move with the first pass
+    // into its bucket order, where k_permute gathers them (ReqRec<false>)
+    const uint4* rec_in = xs ? nullptr : static_cast<const uint4*>(B.rec);
+    uint4* rec_out = xs ? nullptr : static_cast<uint4*>(B.recb);
     if (P <= 1) {
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
                                                        B.ctrl + CTRL_TILE, e->d_eflags, nullptr, nullptr, 0, nullptr,
-                                                       mdev);
+                                                       mdev, rec_in, rec_out);
         kin = B.sk1;
         vin = B.sv1;
     } else {
@@ -1026,7 +1033,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         uint32_t* plan = B.ctrl + CTRL_PLAN;
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(B.sk0, B.sv0, B.sk1, B.sv1, m, e->sort_bits - 8, ghist,
                                                        B.status, B.ctrl + CTRL_TILE, e->d_eflags, nullptr, plan,
-                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr, mdev);
+                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr, mdev, rec_in, rec_out);
         const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
         uint32_t* fk = odd ? B.sk0 : B.sk1;
         uint32_t* fv = odd ? B.sv0 : B.sv1;
@@ -1074,14 +1081,19 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // front_done rides on k_permute's dispatch packet (no marker packet)
     // unless a stamp kernel follows it
     const bool bind_front = !sr;
+    // the arrival index of every sorted position for the finish: the sort's
+    // values (xs), or from the moved records into the free value buffer
+    uint32_t* vfin = xs ? vin : (vin == B.sv0 ? B.sv1 : B.sv0);
     if (xs)
         hipExtLaunchKernelGGL(k_permute<true>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre, mdev);
+                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre, mdev,
+                              a.cfg, (uint32_t*)nullptr);
     else
         hipExtLaunchKernelGGL(k_permute<false>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<false>*>(B.rec), a.n, ps, pre, mdev);
+                              e->d_cfg, e->profile, static_cast<const ReqRec<false>*>(B.recb), a.n, ps, pre, mdev,
+                              a.cfg, vfin);
     if (tall) (void)hipEventRecord(ev[3], f);
     if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 1);
     if (!bind_front) HIPCHK(e, hipEventRecord(B.front_done, f));
@@ -1134,15 +1146,15 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         m, B.runs, e->profile, ps, pre, e->d_eflags);
     if (ri) {
         // a routed batch: one result record per request at its receive index
-        k_unpermute_routed<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->d_cfg, ps, *ri);
+        k_unpermute_routed<<<pgrid, 256, GROUP_LDS, t>>>(kin, vfin, m, e->invalid_key, e->d_cfg, ps, *ri);
     } else if (m <= UP_MAX) {
         // results to the caller's order through arrival-index buckets: no
         // scattered partial-line stores
         k_unpermute_bucket<<<(m + 256 * UP_ITEMS - 1) / (256 * UP_ITEMS), 256, GROUP_LDS, t>>>(
-            kin, vin, m, e->invalid_key, ps, B.upb, B.ctrl + CTRL_UPB);
+            kin, vfin, m, e->invalid_key, ps, B.upb, B.ctrl + CTRL_UPB);
         k_unpermute_bucket_out<<<(m + UP_BUCKET - 1) / UP_BUCKET, 256, 0, t>>>(m, B.upb, e->d_cfg, a);
     } else {
-        k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vin, m, e->invalid_key, e->d_cfg, ps, a);
+        k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vfin, m, e->invalid_key, e->d_cfg, ps, a);
     }
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 5);
     if (e->timing) {

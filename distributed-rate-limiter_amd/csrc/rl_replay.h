@@ -990,24 +990,33 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
 // is read from the caller's array) -- and the clock is floor(ts / 1e6); with
 // one (XS, the routed path's store clock) it is 32 bytes.
 template <bool XS> struct ReqRec;
+// 16 bytes: the record also carries its arrival index, because the grouping
+// sort's first (MSD) pass moves it into bucket order (k_sort_pass rin/rout),
+// where k_permute gathers it from an L2-resident bucket instead of from the
+// whole batch; config and n take 16 bits each (REC_WIDE: read the caller's
+// array at the arrival index)
 template <> struct alignas(16) ReqRec<false> {
     int64_t ts;
-    uint32_t cfg, n32;
+    uint32_t ix;       // arrival index
+    uint32_t cn;       // config id << 16 | n
 };
 template <> struct alignas(32) ReqRec<true> {
     int64_t ts, n, sms;
     uint32_t cfg, pad;
 };
-constexpr uint32_t REC_N_WIDE = 0xffffffffu;   // n32: n does not fit (read the caller's n)
+constexpr uint32_t REC_WIDE = 0xffffu;   // a 16-bit field that does not fit
 static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 32, "request records");
 
 template <bool XS>
-__device__ inline ReqRec<XS> rec_pack(int64_t t, int64_t n, int64_t sms, uint32_t c) {
+__device__ inline ReqRec<XS> rec_pack(int64_t t, int64_t n, int64_t sms, uint32_t c, uint32_t i) {
     if constexpr (XS) {
+        (void)i;
         return ReqRec<true>{t, n, sms, c, 0u};
     } else {
         (void)sms;
-        return ReqRec<false>{t, c, (n > 0 && n < (int64_t)REC_N_WIDE) ? (uint32_t)n : REC_N_WIDE};
+        const uint32_t c16 = c < REC_WIDE ? c : REC_WIDE;
+        const uint32_t n16 = (n > 0 && n < (int64_t)REC_WIDE) ? (uint32_t)n : REC_WIDE;
+        return ReqRec<false>{t, i, (c16 << 16) | n16};
     }
 }
 template <bool XS>
@@ -1016,7 +1025,18 @@ __device__ inline int64_t rec_n(const ReqRec<XS>& r, const int64_t* __restrict__
         (void)n_in; (void)i;
         return r.n;
     } else {
-        return r.n32 != REC_N_WIDE ? (int64_t)r.n32 : n_in[i];
+        const uint32_t n16 = r.cn & 0xffffu;
+        return n16 != REC_WIDE ? (int64_t)n16 : n_in[i];
+    }
+}
+template <bool XS>
+__device__ inline uint32_t rec_cfg(const ReqRec<XS>& r, const uint32_t* __restrict__ cfg_in, uint32_t i) {
+    if constexpr (XS) {
+        (void)cfg_in; (void)i;
+        return r.cfg;
+    } else {
+        const uint32_t c16 = r.cn >> 16;
+        return c16 != REC_WIDE ? c16 : cfg_in[i];
     }
 }
 template <bool XS>
@@ -1028,44 +1048,61 @@ __device__ inline int64_t rec_sms(const ReqRec<XS>& r) {
 // requests to sorted order + the state-free token-bucket precomputation.
 // Each wave covers 64 consecutive sorted positions; a request's predecessor
 // in its segment (position j-1) is the neighbouring lane's record, so only
-// lane 0 gathers a second one.  n_in: the caller's n (arrival order), for a
-// record whose n did not fit.
+// lane 0 gathers a second one.  n_in / cfg_in: the caller's n and config
+// (arrival order), for a record whose field did not fit.
+// !XS: the records are in the MSD pass's bucket order and sv holds each
+// element's position there (the sort carried it), so consecutive sorted
+// positions gather from one bucket's few-KB range (L2) instead of the whole
+// batch; the arrival index comes from the record and goes to ix_out[j] (the
+// finish reads it there).  XS (32-byte records with a server clock, the
+// routed path): sv holds arrival indices and the records stay in arrival order.
 template <bool XS>
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
                                                  const CfgDev* __restrict__ cfgs, int32_t profile,
                                                  const ReqRec<XS>* __restrict__ rec, const int64_t* __restrict__ n_in,
-                                                 ReqArgs out, TbPre pre, const uint32_t* mdev = nullptr) {
+                                                 ReqArgs out, TbPre pre, const uint32_t* mdev,
+                                                 const uint32_t* __restrict__ cfg_in, uint32_t* __restrict__ ix_out) {
     if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < m; base += stride) {
         const uint32_t j = base + lane;
         const uint32_t k0 = j < m ? sk[j] : invalid_key;
-        const uint32_t ix = k0 != invalid_key ? sv[j] : 0u;
+        // XS: the arrival index; else the record's position in bucket order
+        // (read for every element: the finish needs every arrival index)
+        const uint32_t at = (XS ? k0 != invalid_key : j < m) ? sv[j] : 0u;
         // lane 0: the predecessor at j-1 (a previous chunk's last lane)
-        uint32_t kpl = invalid_key, ixp = 0u;
+        uint32_t kpl = invalid_key, atp = 0u;
         if (lane == 0 && j > 0 && k0 != invalid_key && k0 < win_base) {
             kpl = sk[j - 1];
-            if (kpl == k0) ixp = sv[j - 1];
+            if (kpl == k0) atp = sv[j - 1];
         }
         ReqRec<XS> r{}, q{};
-        if (k0 != invalid_key) r = rec[ix];
-        if (lane == 0 && kpl == k0 && k0 != invalid_key) q = rec[ixp];
+        if (XS ? k0 != invalid_key : j < m) r = rec[at];
+        if (lane == 0 && kpl == k0 && k0 != invalid_key) q = rec[atp];
+        uint32_t ix = at;
+        if constexpr (!XS) {
+            ix = r.ix;
+            if (j < m) ix_out[j] = ix;
+        }
         const bool valid = k0 != invalid_key;
         const int64_t sms = rec_sms<XS>(r);
         // predecessor (j-1) fields from the lane below
+        const uint32_t rc = valid ? rec_cfg<XS>(r, cfg_in, ix) : 0u;
         uint32_t kp = __shfl_up(k0, 1);
         int64_t tp = __shfl_up(r.ts, 1);
         int64_t smsp = __shfl_up(sms, 1);
-        uint32_t cp = __shfl_up(r.cfg, 1);
+        uint32_t cp = __shfl_up(rc, 1);
         if (lane == 0) {
             kp = invalid_key;
             if (kpl == k0 && valid) {
                 kp = k0;
                 tp = q.ts;
                 smsp = rec_sms<XS>(q);
-                cp = q.cfg;
+                uint32_t qix = atp;
+                if constexpr (!XS) qix = q.ix;
+                cp = rec_cfg<XS>(q, cfg_in, qix);
             }
         }
         if (!valid) continue;
@@ -1073,10 +1110,10 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
         // `out` is the engine's own permuted buffers (ReqArgs keeps inputs const)
         const_cast<int64_t*>(out.ts)[j] = r.ts;
         const_cast<int64_t*>(out.n)[j] = nn;
-        const_cast<uint32_t*>(out.cfg)[j] = r.cfg;
+        const_cast<uint32_t*>(out.cfg)[j] = rc;
         if (XS) const_cast<int64_t*>(out.sms)[j] = sms;   // only an explicit server clock
         if (k0 >= win_base) continue;
-        const CfgDev& C = cfgs[r.cfg];
+        const CfgDev& C = cfgs[rc];
         const double now = (double)r.ts / 1e9;
         // state-free: a head's add needs the table (tb_head_add, at replay)
         // and the table is still being updated by the previous batch; a

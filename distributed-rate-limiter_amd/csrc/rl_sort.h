@@ -69,6 +69,10 @@ __device__ inline uint32_t block_excl_scan_256(uint32_t v, uint32_t* s_tmp /*[4]
 // skip (nullable): a device flag that turns the pass into a no-op.
 // mdev (nullable): the batch size in device memory, at most m (the grid is
 // sized for m; tiles past the device size exit at once).
+// rin / rout (FIRST only, nullable): 16-byte records in input order, moved
+// along with the keys -- rout[pos] = rin[idx] -- and the value written is the
+// output position itself, so later passes carry each element's position in
+// this pass's output (where its record now is).
 // plan (nullable, the MSD pass of the grouping sort): the block of tile 0
 // writes plan[0] = 1 when no digit of this pass holds more than plan_cap
 // elements (every bucket then fits k_sort_local) and plan[1] = 1 otherwise,
@@ -78,7 +82,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin, uint32_t* __restrict__ kout,
     uint32_t* __restrict__ vout, uint32_t m, int shift, const uint32_t* __restrict__ ghist,
     uint32_t* status, uint32_t* tile_ctr, uint32_t* eflags, const uint32_t* skip = nullptr,
-    uint32_t* plan = nullptr, uint32_t plan_cap = 0, uint32_t* plan_host = nullptr, const uint32_t* mdev = nullptr) {
+    uint32_t* plan = nullptr, uint32_t plan_cap = 0, uint32_t* plan_host = nullptr, const uint32_t* mdev = nullptr,
+    const uint4* __restrict__ rin = nullptr, uint4* __restrict__ rout = nullptr) {
     if (skip && *skip) return;
     if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path): m is its bound
     __shared__ uint32_t s_wcnt[SORT_WAVES][RADIX];
@@ -182,7 +187,12 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
             uint32_t d = (key[j] >> shift) & (RADIX - 1);
             uint32_t pos = s_goff[d] + s_wcnt[wave][d] + rank[j];
             kout[pos] = key[j];
-            vout[pos] = val[j];
+            if (FIRST && rout) {
+                vout[pos] = pos;
+                rout[pos] = rin[idx];
+            } else {
+                vout[pos] = val[j];
+            }
         }
     }
     __syncthreads();   // s_tile, s_wcnt, s_goff, s_tmp are rewritten by the next tile
