@@ -75,6 +75,10 @@ __device__ inline int ch_producer_index(uint32_t wave) {
 }
 constexpr int CH_BLOCK = (CH_NP + 2) * 64;
 constexpr int CH_SERIAL = 64;                          // serial exact steps per round at most
+#ifndef RL_CH_UNCHECKED
+#define RL_CH_UNCHECKED 2
+#endif
+constexpr int CH_UNCHECKED = RL_CH_UNCHECKED;          // near fixed-point passes before the first convergence test
 #ifndef RL_HEAVY_G
 #define RL_HEAVY_G 2
 #endif
@@ -742,9 +746,17 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 const int32_t incl = (int32_t)wave_scan_u32((uint32_t)flip, 0u,
                                                             [](uint32_t x, uint32_t y) { return x + y; });
                 const int32_t en = incl - flip;
+                iters++;
+                // the first CH_UNCHECKED passes skip the convergence test (two
+                // ballots, their scalar first-lane searches and a branch: about
+                // half of a pass's latency): a pass past the fixed point
+                // changes nothing, and most groups need several passes
+                if (it + 1 < CH_UNCHECKED) {
+                    est = en;
+                    continue;
+                }
                 const uint32_t fb = first_lane(__ballot(brk));
                 const uint32_t fc = first_lane(__ballot(v && en != est));
-                iters++;
                 if (fc >= fb) { stop_lane = fb; break; }             // converged up to the first exit
                 if (it + 1 == ITMAX) { stop_lane = fc; break; }      // lanes < fc are exact
                 est = en;
