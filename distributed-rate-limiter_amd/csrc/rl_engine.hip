@@ -141,9 +141,17 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
     uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
     uint32_t* __restrict__ sk, uint32_t* ghist, int passes, uint32_t shifts, ReqArgs a,
-    ReqRec<XS>* __restrict__ rec, uint32_t* eflags, RouteIn ri) {
+    ReqRec<XS>* __restrict__ rec, uint32_t* eflags, RouteIn ri, uint32_t* head, uint32_t nhead) {
     static_assert(!RT || XS, "a routed batch carries its store clock");
+    // the batch set's head words (rl_engine.hip CTRL_HEAD), before any later
+    // kernel of the batch touches them
+    if (blockIdx.x == 0)
+        for (uint32_t k = threadIdx.x; k < nhead; k += PROBE_BLOCK) head[k] = 0u;
     if (RT) m = min(m, *ri.count);
+    // a routed batch in received order (RL_ORDER_IDENTITY): request i is
+    // rec[i], its store clock from its ts and the clock of the earlier steps
+    const bool ident = RT && m && ri.order[0] == RL_ORDER_IDENTITY;
+    const int64_t clock0 = ident ? a.sms[0] : 0;
     __shared__ uint32_t lh[4][RADIX];
     for (int p = 0; p < 4; p++) lh[p][threadIdx.x] = 0;
     __syncthreads();
@@ -160,18 +168,24 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             const bool v = i < m;
             if (RT) {
                 rl_route_rec q{};
-                if (v) q = ri.rec[ri.order[i]];
+                if (v) q = ri.rec[ident ? i : ri.order[i]];
                 k[r] = v ? q.key : EMPTY_KEY;
                 c[r] = q.cfg;
                 nn[r] = q.n;
                 t[r] = q.ts;
+                if (ident) {
+                    const int64_t ms = floor_div(q.ts, 1000000LL);
+                    sms[r] = ms > clock0 ? ms : clock0;
+                } else {
+                    sms[r] = v ? a.sms[i] : 0;
+                }
             } else {
                 k[r] = v ? key[i] : EMPTY_KEY;
                 c[r] = v ? cfg[i] : 0u;
                 nn[r] = v ? n[i] : 0;
                 t[r] = v ? a.ts[i] : 0;
+                sms[r] = v && XS ? a.sms[i] : 0;
             }
-            sms[r] = v && XS ? a.sms[i] : 0;
         }
 #pragma unroll
         for (int r = 0; r < PROBE_R; r++) {   // first probes, all in flight
@@ -393,6 +407,7 @@ __global__ __launch_bounds__(256) void k_unpermute_routed(const uint32_t* __rest
                                                           uint32_t invalid_key, const CfgDev* __restrict__ cfgs,
                                                           ReqArgs sorted, RouteIn ri) {
     m = min(m, *ri.count);
+    const bool ident = m && ri.order[0] == RL_ORDER_IDENTITY;
     for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
         const uint32_t k0 = sk[j];
         const uint32_t p = sv[j];
@@ -403,7 +418,7 @@ __global__ __launch_bounds__(256) void k_unpermute_routed(const uint32_t* __rest
             dec = sorted.dec[j];
             finish_result(dec, sorted.tok[j], sorted.ts[j], sorted.n[j], cfgs[sorted.cfg[j]], rem, retry, reset, tok);
         }
-        ri.res[ri.order[p]] = rl_route_res{(int64_t)dec, rem, retry, reset};
+        ri.res[ident ? p : ri.order[p]] = rl_route_res{(int64_t)dec, rem, retry, reset};
     }
 }
 
@@ -425,15 +440,21 @@ constexpr int NSTAGES = 5;
 constexpr uint32_t STAMP_RING = 256;
 constexpr int NSETS = 3;          // batch buffer sets: grouping b+1 | replay b | finish b-1
 constexpr int GROUP_LDS = 4096;   // LDS floor of the grouping / finish kernels (see rl_engine::chain_pad)
-constexpr uint32_t CTRL_HIST = 0;              // [4][256]
-constexpr uint32_t CTRL_TILE = 4 * RADIX;      // [4] tile counters
-constexpr uint32_t CTRL_NSEG = CTRL_TILE + 4;  // [0..3] list counts (heavy TB, light, heavy window, huge TB)
+// A set's zeroed words.  The head (list counts, queues, diagnostics) is read
+// by the host after the batch (rl_engine_stats), so k_probe zeroes it when the
+// set is next used; everything after it is zeroed on the finish stream as the
+// batch ends (the next use of the set waits for that), so the grouping stream
+// carries no memset.
+constexpr uint32_t CTRL_NSEG = 0;              // [0..3] list counts (heavy TB, light, heavy window, huge TB)
                                                // [4] chain queue [5] per-thread queue [6] per-wave queue
 constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iterations [2] max rounds
                                                // [3..6] round ends (full, stop, partial, first window)
                                                // [8..19] timers [20] exact tiles [21] serial steps
 constexpr uint32_t CTRL_DBGN = 88;
-constexpr uint32_t CTRL_UPB = CTRL_DBG + CTRL_DBGN;   // [UP_NB] bucket fill counters (k_unpermute_bucket)
+constexpr uint32_t CTRL_HEAD = CTRL_DBG + CTRL_DBGN;  // words zeroed by k_probe
+constexpr uint32_t CTRL_HIST = CTRL_HEAD;             // [4][256]
+constexpr uint32_t CTRL_TILE = CTRL_HIST + 4 * RADIX;  // [4] tile counters
+constexpr uint32_t CTRL_UPB = CTRL_TILE + 4;          // [UP_NB] bucket fill counters (k_unpermute_bucket)
 constexpr uint32_t CTRL_PLAN = CTRL_UPB + UP_NB;      // [0] every MSD bucket fits k_sort_local [1] it does not
 constexpr uint32_t CTRL_WORDS = CTRL_PLAN + 2;
 
@@ -478,13 +499,14 @@ struct BatchSet {
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
     void* rec = nullptr;          // requests packed in arrival order (k_probe -> k_permute): ReqRec<XS>
-    void* recb = nullptr;         // ReqRec<false> in the MSD pass's bucket order (k_sort_pass -> k_permute)
+    void* recb = nullptr;         // ReqRec<XS> in the MSD pass's bucket order (k_sort_pass -> k_permute)
     uint8_t* o_dec = nullptr;
     double* o_tok = nullptr;      // tokens (token bucket) / Remaining bits (window): finish_result
     // token-bucket precomputation (k_permute)
     double *q_add = nullptr, *q_th = nullptr;
     TbRuns runs{};                // the chain's committed runs (by start position)
-    uint32_t* zero = nullptr;     // ctrl words + look-back status + huge claims (memset per batch)
+    uint32_t* zero = nullptr;     // ctrl words + look-back status + huge claims (zeroed per batch)
+    bool dirty = false;           // a batch began on the set and did not reach its finish's zeroing
     uint32_t* ctrl = nullptr;
     uint32_t* status = nullptr;
     uint32_t* claim = nullptr;
@@ -644,7 +666,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
     ok &= hipMalloc(&B.rec, sizeof(ReqRec<true>) * M) == hipSuccess;
-    ok &= hipMalloc(&B.recb, sizeof(ReqRec<false>) * M) == hipSuccess;
+    ok &= hipMalloc(&B.recb, sizeof(ReqRec<true>) * M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
     ok &= hipMalloc(&B.o_tok, 8 * M) == hipSuccess;
     // q_add and q_th carry 128 elements of slack: the chain's loader wave
@@ -669,7 +691,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     B.status = B.zero + CTRL_WORDS;
     B.claim = B.status + status_words;
     // run lengths start at 0; k_tb_expand clears every one it consumes
-    return hipMemset(B.runs.len, 0, 2 * M) == hipSuccess;
+    return hipMemset(B.runs.len, 0, 2 * M) == hipSuccess && hipMemset(B.zero, 0, zero_bytes) == hipSuccess;
 }
 
 static void free_all(rl_engine* e) {
@@ -983,7 +1005,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // front start / end, replay start / end, finish start / end
     uint32_t* sr = e->stamp_ring ? e->stamp_ring + 6 * (e->stats.batches % STAMP_RING) : nullptr;
     if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 0);
-    HIPCHK(e, hipMemsetAsync(B.zero, 0, e->zero_bytes, f));
+    if (B.dirty) HIPCHK(e, hipMemsetAsync(B.zero, 0, e->zero_bytes, f));   // an earlier batch stopped early
+    B.dirty = true;
     uint32_t* ghist = B.ctrl + CTRL_HIST;
     // few enough blocks that the per-block histogram flush (3 x 256 global
     // atomics per block on 768 shared words) stays cheap
@@ -998,17 +1021,17 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         k_probe<1, true, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin);
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD);
     else if (xs)
         k_probe<1, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin);
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD);
     else
         k_probe<1, false><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<false>*>(B.rec), e->d_eflags, rin);
+            static_cast<ReqRec<false>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD);
     if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
@@ -1016,14 +1039,15 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     uint32_t* segctr = B.ctrl + CTRL_NSEG;
     const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
-    // 16-byte records (no explicit server clock) move with the first pass
-    // into its bucket order, where k_permute gathers them (ReqRec<false>)
-    const uint4* rec_in = xs ? nullptr : static_cast<const uint4*>(B.rec);
-    uint4* rec_out = xs ? nullptr : static_cast<uint4*>(B.recb);
+    // the request records move with the first pass into its bucket order,
+    // where k_permute gathers them (ReqRec: 16 bytes, 32 with a server clock)
+    const uint4* rec_in = static_cast<const uint4*>(B.rec);
+    uint4* rec_out = static_cast<uint4*>(B.recb);
+    const int rw = xs ? 2 : 1;
     if (P <= 1) {
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
                                                        B.ctrl + CTRL_TILE, e->d_eflags, nullptr, nullptr, 0, nullptr,
-                                                       mdev, rec_in, rec_out);
+                                                       mdev, rec_in, rec_out, rw);
         kin = B.sk1;
         vin = B.sv1;
     } else {
@@ -1033,7 +1057,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         uint32_t* plan = B.ctrl + CTRL_PLAN;
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(B.sk0, B.sv0, B.sk1, B.sv1, m, e->sort_bits - 8, ghist,
                                                        B.status, B.ctrl + CTRL_TILE, e->d_eflags, nullptr, plan,
-                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr, mdev, rec_in, rec_out);
+                                                       LOC_MAX, m > LOC_MAX ? e->d_plan : nullptr, mdev, rec_in, rec_out, rw);
         const bool odd = ((P - 1) & 1) != 0;     // LSD passes after the MSD pass end in sk0 when odd
         uint32_t* fk = odd ? B.sk0 : B.sk1;
         uint32_t* fv = odd ? B.sv0 : B.sv1;
@@ -1081,14 +1105,14 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // front_done rides on k_permute's dispatch packet (no marker packet)
     // unless a stamp kernel follows it
     const bool bind_front = !sr;
-    // the arrival index of every sorted position for the finish: the sort's
-    // values (xs), or from the moved records into the free value buffer
-    uint32_t* vfin = xs ? vin : (vin == B.sv0 ? B.sv1 : B.sv0);
+    // the arrival index of every sorted position for the finish: from the
+    // moved records into the free value buffer
+    uint32_t* vfin = vin == B.sv0 ? B.sv1 : B.sv0;
     if (xs)
         hipExtLaunchKernelGGL(k_permute<true>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre, mdev,
-                              a.cfg, (uint32_t*)nullptr);
+                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.recb), a.n, ps, pre, mdev,
+                              a.cfg, vfin);
     else
         hipExtLaunchKernelGGL(k_permute<false>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
@@ -1146,6 +1170,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         m, B.runs, e->profile, ps, pre, e->d_eflags);
     if (ri) {
         // a routed batch: one result record per request at its receive index
+        // (measured: through merge-position buckets as below it took 107 us
+        // per 1M-request step against this kernel's 64)
         k_unpermute_routed<<<pgrid, 256, GROUP_LDS, t>>>(kin, vfin, m, e->invalid_key, e->d_cfg, ps, *ri);
     } else if (m <= UP_MAX) {
         // results to the caller's order through arrival-index buckets: no
@@ -1161,6 +1187,9 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         if (tall) (void)hipEventRecord(ev[7], t);
         e->ev_pending.push_back(ev);
     }
+    // the set's words for its next batch (all but the head: k_probe)
+    HIPCHK(e, hipMemsetAsync(B.zero + CTRL_HEAD, 0, e->zero_bytes - 4 * CTRL_HEAD, t));
+    B.dirty = false;
     HIPCHK(e, hipEventRecord(B.back_done, t));
     HIPCHK(e, hipStreamWaitEvent(s, B.back_done, 0));
     B.used = true;

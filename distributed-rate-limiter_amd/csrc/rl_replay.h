@@ -988,13 +988,13 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
 // elements.  Without an explicit server clock (XS false, the common case) the
 // record is 16 bytes -- time, config and n when it fits 32 bits (a larger n
 // is read from the caller's array) -- and the clock is floor(ts / 1e6); with
-// one (XS, the routed path's store clock) it is 32 bytes.
+// one (XS, the routed path's store clock) it is 32 bytes.  Either carries its
+// arrival index, because the grouping sort's first (MSD) pass moves it into
+// bucket order (k_sort_pass rin/rout), where k_permute gathers it from an
+// L2-resident bucket instead of from the whole batch.
 template <bool XS> struct ReqRec;
-// 16 bytes: the record also carries its arrival index, because the grouping
-// sort's first (MSD) pass moves it into bucket order (k_sort_pass rin/rout),
-// where k_permute gathers it from an L2-resident bucket instead of from the
-// whole batch; config and n take 16 bits each (REC_WIDE: read the caller's
-// array at the arrival index)
+// 16 bytes: config and n take 16 bits each (REC_WIDE: read the caller's array
+// at the arrival index)
 template <> struct alignas(16) ReqRec<false> {
     int64_t ts;
     uint32_t ix;       // arrival index
@@ -1002,7 +1002,8 @@ template <> struct alignas(16) ReqRec<false> {
 };
 template <> struct alignas(32) ReqRec<true> {
     int64_t ts, n, sms;
-    uint32_t cfg, pad;
+    uint32_t cfg;
+    uint32_t ix;       // arrival index
 };
 constexpr uint32_t REC_WIDE = 0xffffu;   // a 16-bit field that does not fit
 static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 32, "request records");
@@ -1010,8 +1011,7 @@ static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 32, "reques
 template <bool XS>
 __device__ inline ReqRec<XS> rec_pack(int64_t t, int64_t n, int64_t sms, uint32_t c, uint32_t i) {
     if constexpr (XS) {
-        (void)i;
-        return ReqRec<true>{t, n, sms, c, 0u};
+        return ReqRec<true>{t, n, sms, c, i};
     } else {
         (void)sms;
         const uint32_t c16 = c < REC_WIDE ? c : REC_WIDE;
@@ -1050,12 +1050,11 @@ __device__ inline int64_t rec_sms(const ReqRec<XS>& r) {
 // in its segment (position j-1) is the neighbouring lane's record, so only
 // lane 0 gathers a second one.  n_in / cfg_in: the caller's n and config
 // (arrival order), for a record whose field did not fit.
-// !XS: the records are in the MSD pass's bucket order and sv holds each
-// element's position there (the sort carried it), so consecutive sorted
-// positions gather from one bucket's few-KB range (L2) instead of the whole
-// batch; the arrival index comes from the record and goes to ix_out[j] (the
-// finish reads it there).  XS (32-byte records with a server clock, the
-// routed path): sv holds arrival indices and the records stay in arrival order.
+// The records are in the MSD pass's bucket order and sv holds each element's
+// position there (the sort carried it), so consecutive sorted positions
+// gather from one bucket's few-KB range (L2) instead of the whole batch; the
+// arrival index comes from the record and goes to ix_out[j] (the finish reads
+// it there).
 template <bool XS>
 __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk, const uint32_t* __restrict__ sv,
                                                  uint32_t m, uint32_t invalid_key, uint32_t win_base,
@@ -1069,9 +1068,9 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
     for (uint32_t base = blockIdx.x * blockDim.x + (threadIdx.x & ~63u); base < m; base += stride) {
         const uint32_t j = base + lane;
         const uint32_t k0 = j < m ? sk[j] : invalid_key;
-        // XS: the arrival index; else the record's position in bucket order
-        // (read for every element: the finish needs every arrival index)
-        const uint32_t at = (XS ? k0 != invalid_key : j < m) ? sv[j] : 0u;
+        // the record's position in bucket order (read for every element: the
+        // finish needs every arrival index)
+        const uint32_t at = j < m ? sv[j] : 0u;
         // lane 0: the predecessor at j-1 (a previous chunk's last lane)
         uint32_t kpl = invalid_key, atp = 0u;
         if (lane == 0 && j > 0 && k0 != invalid_key && k0 < win_base) {
@@ -1079,13 +1078,10 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
             if (kpl == k0) atp = sv[j - 1];
         }
         ReqRec<XS> r{}, q{};
-        if (XS ? k0 != invalid_key : j < m) r = rec[at];
+        if (j < m) r = rec[at];
         if (lane == 0 && kpl == k0 && k0 != invalid_key) q = rec[atp];
-        uint32_t ix = at;
-        if constexpr (!XS) {
-            ix = r.ix;
-            if (j < m) ix_out[j] = ix;
-        }
+        const uint32_t ix = r.ix;
+        if (j < m) ix_out[j] = ix;
         const bool valid = k0 != invalid_key;
         const int64_t sms = rec_sms<XS>(r);
         // predecessor (j-1) fields from the lane below
@@ -1100,9 +1096,7 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
                 kp = k0;
                 tp = q.ts;
                 smsp = rec_sms<XS>(q);
-                uint32_t qix = atp;
-                if constexpr (!XS) qix = q.ix;
-                cp = rec_cfg<XS>(q, cfg_in, qix);
+                cp = rec_cfg<XS>(q, cfg_in, q.ix);
             }
         }
         if (!valid) continue;

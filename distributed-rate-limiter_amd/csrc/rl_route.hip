@@ -324,7 +324,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_bm_tmax(const rl_route_rec* __rest
 // the same info rows, so every owner keeps the same clock
 __global__ __launch_bounds__(1024) void k_bm_tscan(const int64_t* __restrict__ info, uint32_t world, uint32_t cap,
                                                    uint32_t tps, unsigned long long* tmax, int64_t* clock,
-                                                   MergeCtl* ctl, uint32_t* count) {
+                                                   MergeCtl* ctl, uint32_t* count, uint32_t* order, int64_t* sms) {
     __shared__ unsigned long long s_w[16];
     __shared__ unsigned long long s_carry;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -369,12 +369,19 @@ __global__ __launch_bounds__(1024) void k_bm_tscan(const int64_t* __restrict__ i
         ctl->clock_prev = c0;
         *clock = c1;
         *count = tot;
+        // one source in time order: the received order is the decision order
+        // and each request's clock follows from its own ts (RL_ORDER_IDENTITY)
+        if (world == 1 && recv_sorted(info, 0)) {
+            order[0] = RL_ORDER_IDENTITY;
+            sms[0] = c0;
+        }
     }
 }
 
 // every received record's arrival (biased): the running max of its source's
 // ts so far.  One source (world 1): the received order is the decision order,
-// so the order and store clocks are written here and nothing else runs.
+// so the order and store clocks are written here and nothing else runs (and
+// nothing at all for one source in time order: RL_ORDER_IDENTITY).
 __global__ __launch_bounds__(RT_BLOCK) void k_bm_keys(const rl_route_rec* __restrict__ rec,
                                                       const int64_t* __restrict__ info, uint32_t world, uint32_t cap,
                                                       uint32_t tps, const unsigned long long* __restrict__ tpre,
@@ -385,6 +392,7 @@ __global__ __launch_bounds__(RT_BLOCK) void k_bm_keys(const rl_route_rec* __rest
     const uint32_t s = blockIdx.x / tps, u = blockIdx.x % tps;
     const uint32_t c = recv_count(info, s, cap);
     if (u * MT_TILE >= c) return;   // block-uniform
+    if (world == 1 && recv_sorted(info, 0)) return;   // RL_ORDER_IDENTITY (k_bm_tscan)
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t i0 = u * MT_TILE + threadIdx.x * MT_ITEMS;
     const bool sorted = recv_sorted(info, s);    // block-uniform
@@ -681,7 +689,7 @@ extern "C" int rl_route_merge(rl_router* r, const rl_route_rec* recv, const int6
     const uint32_t G = r->world, cap = r->cap;
     const uint32_t tps = cap / MT_TILE;
     k_bm_tmax<<<G * tps, RT_BLOCK, 0, s>>>(recv, recv_info, cap, tps, r->tmax);
-    k_bm_tscan<<<G, 1024, 0, s>>>(recv_info, G, cap, tps, r->tmax, r->d_clock, r->ctl, count);
+    k_bm_tscan<<<G, 1024, 0, s>>>(recv_info, G, cap, tps, r->tmax, r->d_clock, r->ctl, count, order, server_ms);
     k_bm_keys<<<G * tps, RT_BLOCK, 0, s>>>(recv, recv_info, G, cap, tps, r->tmax, r->ctl, r->ak0, order, server_ms);
     // the merge tree: ceil(log2 G) levels, ping-pong between (ak0, iv0) and (ak1, iv1)
     uint32_t levels = 0;

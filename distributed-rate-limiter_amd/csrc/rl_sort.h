@@ -69,8 +69,8 @@ __device__ inline uint32_t block_excl_scan_256(uint32_t v, uint32_t* s_tmp /*[4]
 // skip (nullable): a device flag that turns the pass into a no-op.
 // mdev (nullable): the batch size in device memory, at most m (the grid is
 // sized for m; tiles past the device size exit at once).
-// rin / rout (FIRST only, nullable): 16-byte records in input order, moved
-// along with the keys -- rout[pos] = rin[idx] -- and the value written is the
+// rin / rout (FIRST only, nullable): records of `rw` 16-byte words in input
+// order, moved along with the keys -- rout[pos] = rin[idx] -- and the value written is the
 // output position itself, so later passes carry each element's position in
 // this pass's output (where its record now is).
 // plan (nullable, the MSD pass of the grouping sort): the block of tile 0
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     uint32_t* __restrict__ vout, uint32_t m, int shift, const uint32_t* __restrict__ ghist,
     uint32_t* status, uint32_t* tile_ctr, uint32_t* eflags, const uint32_t* skip = nullptr,
     uint32_t* plan = nullptr, uint32_t plan_cap = 0, uint32_t* plan_host = nullptr, const uint32_t* mdev = nullptr,
-    const uint4* __restrict__ rin = nullptr, uint4* __restrict__ rout = nullptr) {
+    const uint4* __restrict__ rin = nullptr, uint4* __restrict__ rout = nullptr, int rw = 1) {
     if (skip && *skip) return;
     if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path): m is its bound
     __shared__ uint32_t s_wcnt[SORT_WAVES][RADIX];
@@ -189,7 +189,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
             kout[pos] = key[j];
             if (FIRST && rout) {
                 vout[pos] = pos;
-                rout[pos] = rin[idx];
+                for (int w = 0; w < rw; w++) rout[(size_t)pos * rw + w] = rin[(size_t)idx * rw + w];
             } else {
                 vout[pos] = val[j];
             }

@@ -1545,24 +1545,39 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
     if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
     for (;;) {
         // claim the longest unclaimed huge segment (their list is short:
-        // batch / 4096 at most), so the hottest key starts with the first block
-        if (threadIdx.x == 0) {
-            uint32_t got = NO_STOP;
-            if (atomicAdd(&qctr[0], 1u) < nhuge) {
-                for (;;) {
-                    uint32_t best = NO_STOP, blen = 0;
-                    for (uint32_t k = 0; k < nhuge; k++) {
-                        const SegRec r = L.list[3][k];
-                        if (r.len > blen && __hip_atomic_load(&L.claim[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-                            best = k;
-                            blen = r.len;
-                        }
+        // batch / 4096 at most), so the hottest key starts with the first
+        // block.  The block reads the whole list at once (one entry per
+        // thread, an argmax over the waves): one memory round trip, not one
+        // per entry before the hot key's chain can start
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[0], 1u) < nhuge ? 0u : NO_STOP;
+        __syncthreads();
+        if (s_u == 0u) {
+            __shared__ uint64_t s_best[CH_BLOCK / 64];
+            for (;;) {
+                uint64_t best = 0;   // (len << 32) | (~k): the longest, ties to the lowest k
+                for (uint32_t k = threadIdx.x; k < nhuge; k += blockDim.x) {
+                    const uint32_t len = L.list[3][k].len;
+                    if (__hip_atomic_load(&L.claim[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                        const uint64_t c = ((uint64_t)len << 32) | (uint32_t)~k;
+                        best = c > best ? c : best;
                     }
-                    if (best == NO_STOP) break;
-                    if (atomicCAS(&L.claim[best], 0u, 1u) == 0u) { got = best; break; }
                 }
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(best, off);
+                    best = o > best ? o : best;
+                }
+                if ((threadIdx.x & 63) == 0) s_best[threadIdx.x >> 6] = best;
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    uint64_t b = 0;
+                    for (int w = 0; w < CH_BLOCK / 64; w++) b = s_best[w] > b ? s_best[w] : b;
+                    const uint32_t k = ~(uint32_t)b;
+                    s_u = b == 0 ? NO_STOP : (atomicCAS(&L.claim[k], 0u, 1u) == 0u ? k : NO_STOP - 1u);
+                }
+                __syncthreads();
+                if (s_u != NO_STOP - 1u) break;   // claimed one, or none is left; else another block won it: again
+                __syncthreads();
             }
-            s_u = got;
         }
         __syncthreads();
         const uint32_t u = s_u;

@@ -70,6 +70,7 @@ extern "C" {
 #define RL_EOVERFLOW (-75)     /* a request exceeded its owner's bucket capacity (rl_router_sync) */
 #define RL_DROPPED 4           /* decision: not executed, its owner's bucket was full (resubmit it) */
 #define RL_ROUTE_INFO 4        /* int64 per info row: count sent, earliest ts, latest ts, 2 * dropped + unsorted */
+#define RL_ORDER_IDENTITY 0xffffffffu   /* order[0]: the received order is the decision order (rl_route_merge) */
 
 /* one routed request (send and receive buckets) */
 typedef struct rl_route_rec {
@@ -126,8 +127,13 @@ int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts
 /* owner: recv[world * cap] (source s's bucket at s * cap) and recv_info (the
  * received info rows, source s's at RL_ROUTE_INFO * s) -> the decision order:
  * order[p] = receive index of the p-th request, server_ms[p] its store clock,
- * *count = requests received (p < *count are valid).  Call once per step, in
- * step order (it advances the store clock). */
+ * *count = requests received (p < *count are valid).  One source whose batch
+ * is in time order (world 1, info flag clear) is its own decision order: the
+ * merge then writes only order[0] = RL_ORDER_IDENTITY and server_ms[0] = the
+ * store clock of the earlier steps, meaning order[p] = p and server_ms[p] =
+ * max(server_ms[0], floor(recv[p].ts / 1e6)); rl_decide_routed_device reads
+ * that form directly.  Call once per step, in step order (it advances the
+ * store clock). */
 int rl_route_merge(rl_router* r, const rl_route_rec* recv, const int64_t* recv_info, uint32_t* order,
                    int64_t* server_ms, uint32_t* count, void* stream);
 

@@ -73,7 +73,7 @@ def test_route_pack_matches_restatement(rl, world, cap):
     for o in range(world):
         c_o = int(scnt_h[o, 0])
         assert torch.equal(sd[o * C:o * C + c_o], send_h[o * C:o * C + c_o])
-    dropped = int(scnt_h[:, 3].sum())
+    dropped = int((scnt_h[:, 3] >> 1).sum())   # row 3: 2 * dropped + unsorted
     assert (dropped > 0) == ops.overflow
     assert r.sync(s) == (rl.RL_EOVERFLOW if dropped else rl.RL_OK)
     assert r.sync(s) == rl.RL_OK        # sticky until read, then cleared
@@ -137,6 +137,54 @@ def test_route_merge_matches_restatement(rl, world):
         assert int(cnt.cpu()[0]) == int(cnt_h[0]) == tot
         assert torch.equal(order.cpu()[:tot], order_h[:tot])
         assert torch.equal(sms.cpu()[:tot], sms_h[:tot])
+    r.close()
+
+
+def test_route_merge_one_source_in_order_is_identity(rl):
+    """world 1, batches in time order: the merge writes only the identity
+    marker (RL_ORDER_IDENTITY) and the earlier steps' clock, and that form
+    expands to the restatement's order and store clocks; an out-of-order
+    batch in between gets the full order"""
+    import torch
+
+    import route_ops
+    rng = np.random.default_rng(23)
+    r = rl.Router(0, 1, 4096, 4096)
+    ops = route_ops.NumpyRouteOps(1, 4096)
+    C = r.capacity
+    s = torch.cuda.current_stream().cuda_stream
+    for step, (c, in_order) in enumerate([(3000, True), (C, False), (C, True), (0, True), (17, True)]):
+        ts = T0 + step * 2_000_000_000 + rng.integers(0, 3_000_000_000, c).astype(np.int64)
+        if in_order:
+            ts = np.sort(ts)
+        if step == 2:
+            ts = np.minimum(ts, T0)            # times back below the store clock
+        recv = np.zeros((C, 4), np.int64)
+        recv[:c] = np.stack([rng.integers(0, 1 << 62, c), ts, np.ones(c, np.int64),
+                             np.arange(c, dtype=np.int64) << 32], 1)
+        unsorted = int(c > 1 and bool(np.any(ts[1:] < ts[:-1])))
+        info = np.array([[c, ts.min() if c else (1 << 63) - 1, ts.max() if c else -(1 << 63), unsorted]], np.int64)
+        order = torch.full((C,), -7, dtype=torch.int32, device="cuda")
+        sms = torch.empty(C, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        r.merge(torch.from_numpy(recv).cuda().data_ptr(), torch.from_numpy(info).cuda().data_ptr(),
+                order.data_ptr(), sms.data_ptr(), cnt.data_ptr(), s)
+        order_h = torch.empty(C, dtype=torch.int32)
+        sms_h = torch.empty(C, dtype=torch.int64)
+        cnt_h = torch.zeros(1, dtype=torch.int32)
+        ops.merge(torch.from_numpy(recv).data_ptr(), torch.from_numpy(info).data_ptr(), order_h.data_ptr(),
+                  sms_h.data_ptr(), cnt_h.data_ptr(), None)
+        assert r.sync(s) == rl.RL_OK
+        assert int(cnt.cpu()[0]) == int(cnt_h[0]) == c
+        o, sm = order.cpu(), sms.cpu()
+        if in_order:
+            assert int(o[0]) == -1                       # RL_ORDER_IDENTITY as int32
+            o = torch.arange(C, dtype=torch.int32)
+            sm = torch.maximum(torch.from_numpy(recv[:, 1] // 1_000_000), sm[0])
+        else:
+            assert int(o[0]) != -1
+        assert torch.equal(o[:c], order_h[:c])
+        assert torch.equal(sm[:c], sms_h[:c])
     r.close()
 
 
