@@ -201,16 +201,20 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             const uint32_t i = i0 + r * PROBE_BLOCK;
             if (i >= m) continue;
             uint32_t slot = invalid_key;
+            bool ins = false;
             if (go[r]) {
-                const uint32_t s = tbk[r] ? probe_insert_at(tb, tb_mask, k[r], h[r], cur[r])
-                                          : probe_insert_at(win, win_mask, k[r], h[r], cur[r]);
+                const uint32_t s = tbk[r] ? probe_insert_at(tb, tb_mask, k[r], h[r], cur[r], &ins)
+                                          : probe_insert_at(win, win_mask, k[r], h[r], cur[r], &ins);
                 if (s == NO_SLOT) ef |= EF_TABLE_FULL;
                 else slot = tbk[r] ? s : win_base + s;
             }
             sk[i] = slot;
             // one record per request: k_permute's sorted-order gather then
             // touches one line fragment instead of four arrays
-            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r], i);
+            // REC_FRESH: this request inserted its key, so no earlier batch
+            // has it, and a request alone with its key in the batch starts
+            // from the absent state (replay phase 3 then skips the entry read)
+            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r], i | (ins ? REC_FRESH : 0u));
             for (int p = 0; p < passes; p++)
                 atomicAdd(&lh[p][(slot >> ((shifts >> (8 * p)) & 31u)) & (RADIX - 1)], 1u);
         }
@@ -500,6 +504,7 @@ struct BatchSet {
     uint32_t* p_cfg = nullptr;
     void* rec = nullptr;          // requests packed in arrival order (k_probe -> k_permute): ReqRec<XS>
     void* recb = nullptr;         // ReqRec<XS> in the MSD pass's bucket order (k_sort_pass -> k_permute)
+    uint8_t* p_fresh = nullptr;   // sorted order: the request inserted its key (k_permute -> replay phase 3)
     uint8_t* o_dec = nullptr;
     double* o_tok = nullptr;      // tokens (token bucket) / Remaining bits (window): finish_result
     // token-bucket precomputation (k_permute)
@@ -639,6 +644,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.p_ts); (void)hipFree(B.p_n); (void)hipFree(B.p_sms); (void)hipFree(B.p_cfg);
     (void)hipFree(B.rec);
     (void)hipFree(B.recb);
+    (void)hipFree(B.p_fresh);
     (void)hipFree(B.o_dec);
     (void)hipFree(B.o_tok);
     (void)hipFree(B.q_add); (void)hipFree(B.q_th);
@@ -667,6 +673,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
     ok &= hipMalloc(&B.rec, sizeof(ReqRec<true>) * M) == hipSuccess;
     ok &= hipMalloc(&B.recb, sizeof(ReqRec<true>) * M) == hipSuccess;
+    ok &= hipMalloc(&B.p_fresh, M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
     ok &= hipMalloc(&B.o_tok, 8 * M) == hipSuccess;
     // q_add and q_th carry 128 elements of slack: the chain's loader wave
@@ -1098,7 +1105,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // sorted-order buffers; tokens always kept (token-bucket results derive from them)
     // (the server clock only when the caller gave one: else floor(ts / 1e6) where it is read)
     ReqArgs ps{nullptr, B.p_ts, B.p_n, B.p_cfg, a.sms ? B.p_sms : nullptr, B.o_dec, nullptr, nullptr, nullptr,
-               B.o_tok};
+               B.o_tok, B.p_fresh};
     int pgrid = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
     const int pgrid_r = (int)std::min<uint32_t>((m + 255) / 256, (uint32_t)e->perm_grid);
     TbPre pre{B.q_add, B.q_th};

@@ -28,6 +28,7 @@ struct ReqArgs {
     int64_t* retry;
     int64_t* reset;
     double* tok;          // nullable
+    const uint8_t* fresh = nullptr;   // sorted order, nullable: the request inserted its key (REC_FRESH)
 };
 
 // State-independent token-bucket quantities of each request (sorted order),
@@ -143,10 +144,11 @@ __device__ inline double tb_head_add(const TbEntry* e, uint32_t j0, const CfgDev
                                                                           : __builtin_nan("");
 }
 
+// fresh: the batch inserted the key (its entry holds the absent state, not read)
 __device__ inline void replay_tb_serial(TbEntry* e, uint32_t j0, uint32_t j1, const CfgDev* cfgs,
-                                        int32_t profile, const ReqArgs& a, const TbPre& pre) {
-    double tok = e->tok;
-    const double add0 = tb_head_add(e, j0, cfgs, profile, a);
+                                        int32_t profile, const ReqArgs& a, const TbPre& pre, bool fresh = false) {
+    double tok = fresh ? 0.0 : e->tok;
+    const double add0 = fresh ? __builtin_nan("") : tb_head_add(e, j0, cfgs, profile, a);
     for (uint32_t j = j0; j < j1; j++) {
         const double add = j == j0 ? add0 : pre.add[j];
         const bool alive = add == add;
@@ -172,9 +174,20 @@ __device__ inline void replay_win_steps(WinState& w, const Spill& S, uint32_t j0
     }
 }
 
+// fresh: one request on a key the batch inserted -- the absent state, not
+// read (one request on two free slots never reaches the spill, which alone
+// needs the key)
 __device__ inline void replay_win_serial(WinEntry* e, const Spill& S, uint32_t j0, uint32_t j1,
-                                         const CfgDev* cfgs, int32_t profile, const ReqArgs& a, uint32_t* eflags) {
-    WinState w = win_load(e);
+                                         const CfgDev* cfgs, int32_t profile, const ReqArgs& a, uint32_t* eflags,
+                                         bool fresh = false) {
+    WinState w;
+    if (fresh) {
+        w.key = EMPTY_KEY;
+        w.nspill = 0;
+        for (int k = 0; k < 2; k++) w.s[k] = WinSlot{0, 0, ABSENT};
+    } else {
+        w = win_load(e);
+    }
     uint32_t ef = 0;
     replay_win_steps(w, S, j0, j1, cfgs, profile, a, ef);
     win_store(e, w);
@@ -1006,6 +1019,7 @@ template <> struct alignas(32) ReqRec<true> {
     uint32_t ix;       // arrival index
 };
 constexpr uint32_t REC_WIDE = 0xffffu;   // a 16-bit field that does not fit
+constexpr uint32_t REC_FRESH = 1u << 31;  // ix: the request's probe inserted its key (k_probe)
 static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 32, "request records");
 
 template <bool XS>
@@ -1080,8 +1094,11 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
         ReqRec<XS> r{}, q{};
         if (j < m) r = rec[at];
         if (lane == 0 && kpl == k0 && k0 != invalid_key) q = rec[atp];
-        const uint32_t ix = r.ix;
-        if (j < m) ix_out[j] = ix;
+        const uint32_t ix = r.ix & ~REC_FRESH;
+        if (j < m) {
+            ix_out[j] = ix;
+            if (out.fresh) const_cast<uint8_t*>(out.fresh)[j] = (uint8_t)(r.ix >> 31);
+        }
         const bool valid = k0 != invalid_key;
         const int64_t sms = rec_sms<XS>(r);
         // predecessor (j-1) fields from the lane below
@@ -1096,7 +1113,7 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
                 kp = k0;
                 tp = q.ts;
                 smsp = rec_sms<XS>(q);
-                cp = rec_cfg<XS>(q, cfg_in, q.ix);
+                cp = rec_cfg<XS>(q, cfg_in, q.ix & ~REC_FRESH);
             }
         }
         if (!valid) continue;

@@ -86,8 +86,11 @@ __device__ inline uint32_t probe_insert(E* tab, uint64_t mask, uint64_t k) {
 // probe_insert with the first probe's key word already loaded (`cur`, the
 // key at slot h = mix64(k) & mask): lets a thread issue the first loads of
 // several requests before resolving any (memory-level parallelism)
+// (*ins: this call's CAS inserted the key -- its entry holds the initial,
+// absent state: keys are never removed from a table, only rehashed by GC)
 template <typename E>
-__device__ inline uint32_t probe_insert_at(E* tab, uint64_t mask, uint64_t k, uint64_t h, uint64_t cur) {
+__device__ inline uint32_t probe_insert_at(E* tab, uint64_t mask, uint64_t k, uint64_t h, uint64_t cur,
+                                          bool* ins = nullptr) {
     const uint64_t lim = mask < MAX_PROBES ? mask : MAX_PROBES;
     for (uint64_t p = 0; p <= lim; p++) {
         if (p) cur = tab[h].key;
@@ -95,7 +98,10 @@ __device__ inline uint32_t probe_insert_at(E* tab, uint64_t mask, uint64_t k, ui
         if (cur == EMPTY_KEY) {
             unsigned long long prev = atomicCAS((unsigned long long*)&tab[h].key, (unsigned long long)EMPTY_KEY,
                                                 (unsigned long long)k);
-            if (prev == EMPTY_KEY || prev == k) return (uint32_t)h;
+            if (prev == EMPTY_KEY || prev == k) {
+                if (ins) *ins = prev == EMPTY_KEY;
+                return (uint32_t)h;
+            }
         }
         h = (h + 1) & mask;
     }

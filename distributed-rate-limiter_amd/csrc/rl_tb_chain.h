@@ -1632,8 +1632,10 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         if (u < nlight) {
             const SegRec sg = L.list[1][u];
             const uint32_t k0 = sk[sg.j0];
-            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre);
-            else replay_win_serial(&win[k0 - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags);
+            // a key the batch inserted, alone in it: the absent state, unread
+            const bool fresh = sg.len == 1u && a.fresh && a.fresh[sg.j0];
+            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, fresh);
+            else replay_win_serial(&win[k0 - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags, fresh);
         }
     }
     if (threadIdx.x == 0 && dbg) {
