@@ -503,7 +503,7 @@ struct BatchSet {
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
     void* rec = nullptr;          // requests packed in arrival order (k_probe -> k_permute): ReqRec<XS>
-    void* recb = nullptr;         // ReqRec<XS> in the MSD pass's bucket order (k_sort_pass -> k_permute)
+    void* recb = nullptr;         // ReqRec<false> in the MSD pass's bucket order (k_sort_pass -> k_permute)
     uint8_t* p_fresh = nullptr;   // sorted order: the request inserted its key (k_permute -> replay phase 3)
     uint8_t* o_dec = nullptr;
     double* o_tok = nullptr;      // tokens (token bucket) / Remaining bits (window): finish_result
@@ -672,7 +672,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
     ok &= hipMalloc(&B.rec, sizeof(ReqRec<true>) * M) == hipSuccess;
-    ok &= hipMalloc(&B.recb, sizeof(ReqRec<true>) * M) == hipSuccess;
+    ok &= hipMalloc(&B.recb, sizeof(ReqRec<false>) * M) == hipSuccess;
     ok &= hipMalloc(&B.p_fresh, M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
     ok &= hipMalloc(&B.o_tok, 8 * M) == hipSuccess;
@@ -980,8 +980,9 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
 
 // ri (nullable): a routed batch (RouteIn), at most m requests, its size in
 // device memory; its inputs come from `s` (the merge)
+// s_out (nullable): the stream that waits for the results, when not s
 static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool inputs_ready,
-                     const KeyBytes* kb = nullptr, const RouteIn* ri = nullptr) {
+                     const KeyBytes* kb = nullptr, const RouteIn* ri = nullptr, hipStream_t s_out = nullptr) {
     if (m == 0) return RL_OK;
     if (m <= e->small_max && !e->timing && !ri) return run_small(e, m, a, s, inputs_ready, kb);
     const uint32_t* mdev = ri ? ri->count : nullptr;
@@ -1048,9 +1049,12 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
     // the request records move with the first pass into its bucket order,
     // where k_permute gathers them (ReqRec: 16 bytes, 32 with a server clock)
-    const uint4* rec_in = static_cast<const uint4*>(B.rec);
-    uint4* rec_out = static_cast<uint4*>(B.recb);
-    const int rw = xs ? 2 : 1;
+    // (the 32-byte records of an explicit server clock stay in arrival order:
+    // moving them cost the MSD pass more than the permute's gather saves,
+    // 170-250 against 160 us per routed 1M batch, profiles/r4r_rt_prof)
+    const uint4* rec_in = xs ? nullptr : static_cast<const uint4*>(B.rec);
+    uint4* rec_out = xs ? nullptr : static_cast<uint4*>(B.recb);
+    const int rw = 1;
     if (P <= 1) {
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
                                                        B.ctrl + CTRL_TILE, e->d_eflags, nullptr, nullptr, 0, nullptr,
@@ -1118,7 +1122,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (xs)
         hipExtLaunchKernelGGL(k_permute<true>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.recb), a.n, ps, pre, mdev,
+                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre, mdev,
                               a.cfg, vfin);
     else
         hipExtLaunchKernelGGL(k_permute<false>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
@@ -1198,7 +1202,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     HIPCHK(e, hipMemsetAsync(B.zero + CTRL_HEAD, 0, e->zero_bytes - 4 * CTRL_HEAD, t));
     B.dirty = false;
     HIPCHK(e, hipEventRecord(B.back_done, t));
-    HIPCHK(e, hipStreamWaitEvent(s, B.back_done, 0));
+    HIPCHK(e, hipStreamWaitEvent(s_out ? s_out : s, B.back_done, 0));
     B.used = true;
     HIPCHK(e, hipGetLastError());
     e->stats.batches++;
@@ -1293,18 +1297,25 @@ extern "C" int rl_decide_batch_device(rl_engine* e, size_t m, const uint64_t* ke
     return RL_OK;
 }
 
-extern "C" int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
-                                       const uint32_t* order, const int64_t* server_ms, rl_route_res* res,
-                                       void* stream) {
+extern "C" int rl_decide_routed_device_io(rl_engine* e, size_t m_max, const uint32_t* count,
+                                          const rl_route_rec* recv, const uint32_t* order, const int64_t* server_ms,
+                                          rl_route_res* res, void* in_stream, void* out_stream) {
     if (!e || !count || (m_max && (!recv || !order || !server_ms || !res))) return RL_EINVAL;
     if (m_max > e->max_batch) return fail(e, RL_EINVAL, "routed batch bound above max_batch");
     if (!m_max) return RL_OK;
     (void)hipSetDevice(e->device);
-    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    hipStream_t s = in_stream ? (hipStream_t)in_stream : e->stream;
+    hipStream_t so = out_stream ? (hipStream_t)out_stream : s;
     // the server-clock array is the routed records' store clock (always given)
     ReqArgs a{nullptr, nullptr, nullptr, nullptr, server_ms, nullptr, nullptr, nullptr, nullptr, nullptr};
     const RouteIn ri{recv, order, count, res};
-    return run_batch(e, (uint32_t)m_max, a, s, false, nullptr, &ri);
+    return run_batch(e, (uint32_t)m_max, a, s, false, nullptr, &ri, so);
+}
+
+extern "C" int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
+                                       const uint32_t* order, const int64_t* server_ms, rl_route_res* res,
+                                       void* stream) {
+    return rl_decide_routed_device_io(e, m_max, count, recv, order, server_ms, res, stream, stream);
 }
 
 extern "C" int rl_decide_batch_keys_device(rl_engine* e, size_t m, const uint8_t* key_bytes, uint64_t nbytes,

@@ -201,6 +201,7 @@ _sig = {
     "rl_route_merge": (C.c_int, [vp] + [vp] * 6),
     "rl_route_unpack": (C.c_int, [vp, C.c_size_t] + [vp] * 7),
     "rl_decide_routed_device": (C.c_int, [vp, C.c_size_t] + [vp] * 6),
+    "rl_decide_routed_device_io": (C.c_int, [vp, C.c_size_t] + [vp] * 7),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -292,10 +293,16 @@ class Engine:
         out.status = rc
         return out
 
-    def decide_routed(self, m_max, count_p, recv_p, order_p, sms_p, res_p, stream=None):
-        """rl_decide_routed_device (include/rl_route.h): the merged routed
-        batch (its size in device memory at count_p, at most m_max)"""
-        rc = lib.rl_decide_routed_device(self.h, m_max, count_p, recv_p, order_p, sms_p, res_p, stream)
+    def decide_routed(self, m_max, count_p, recv_p, order_p, sms_p, res_p, stream=None, out_stream=None):
+        """rl_decide_routed_device(_io) (include/rl_route.h): the merged
+        routed batch (its size in device memory at count_p, at most m_max);
+        the grouping waits for `stream`, `out_stream` (default: `stream`)
+        waits for the results"""
+        if out_stream is None:
+            rc = lib.rl_decide_routed_device(self.h, m_max, count_p, recv_p, order_p, sms_p, res_p, stream)
+        else:
+            rc = lib.rl_decide_routed_device_io(self.h, m_max, count_p, recv_p, order_p, sms_p, res_p, stream,
+                                                out_stream)
         if rc != RL_OK:
             raise EngineError(rc, self.last_error())
 

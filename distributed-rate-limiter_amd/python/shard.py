@@ -73,15 +73,23 @@ class RoutedPipeline:
     reports RL_EOVERFLOW); size `cap` for the key skew (a uniform hash
     partition needs ~max_batch / world plus a margin, a Zipf hot key more).
 
-    Streams: packs and the request-side collectives run in step order on one
-    request stream R (the router's pack scratch); each step's merge, engine,
-    result all-to-all and unpack on the step's stream (one of `depth`), the
-    merges chained in step order by an event (the router's merge scratch and
-    store clock).  `depth` buffer sets rotate; a set is rewritten only after
-    the step that used it `depth` steps earlier has finished.
+    Streams (two, each on a hardware queue of its own): the request stream R
+    runs every step's pack, request-side collectives and merge in step order
+    (the router's scratch and store clock are sequential) and hands the
+    merged batch to the engine; the result stream U takes the engine's
+    results, runs the result all-to-all and the unpack.  So R goes on with
+    the next step while the engine decides this one.  `depth` buffer sets
+    rotate; a set is rewritten only after the step that used it `depth`
+    steps earlier has unpacked.  (Round 3-4 ran each step's merge, engine
+    call, result exchange and unpack on one of `depth` step streams: with the
+    engine's three streams that made up to nine queues, and the engine's
+    grouping of step b waited for step b - depth's unpack on the same step
+    stream.)
 
-    decide(m_max, count, recv, order, sms, res, stream) runs the owner's
-    engine on the merged batch (rl_decide_routed_device; device pointers).
+    decide(m_max, count, recv, order, sms, res, in_stream, out_stream) runs
+    the owner's engine on the merged batch (rl_decide_routed_device_io;
+    device pointers): the grouping waits for in_stream, out_stream waits for
+    the results.
     exchange: run the collectives (world > 1 always; at world 1 they are
     loopback copies over a one-rank group, e.g. to exercise RCCL; without them
     the buckets and results are read in place)."""
@@ -113,6 +121,7 @@ class RoutedPipeline:
             return mk() if mk is not None else torch.cuda.Stream(d)
 
         self.R = new_stream()
+        self.U = new_stream()
         self.slots = []
         for _ in range(depth):
             s = dict(
@@ -127,10 +136,9 @@ class RoutedPipeline:
                 count=torch.zeros(1, dtype=torch.int32, device=d),
                 res=torch.empty((tot, 4), dtype=torch.int64, device=d),
                 back=torch.empty((tot, 4), dtype=torch.int64, device=d) if self.exchange else None,
-                S=new_stream(), ev_req=None, ev_done=None,
+                ev_done=None,
             )
             self.slots.append(s)
-        self.ev_last_merge = None
         self.collectives = 0          # all-to-alls issued (tests: the exchange really ran)
         self.wait_s = 0.0             # host time spent waiting on the device: none by construction
         self.host_prof = {}
@@ -161,37 +169,28 @@ class RoutedPipeline:
         m = key.numel()
         assert m <= self.max_batch
         p, sp = self._p, self._sp
-        R, S = self.R, s["S"]
+        R, U = self.R, self.U
+        recv = s["recv"] if self.exchange else s["send"]
+        rcnt = s["rcnt"] if self.exchange else s["scnt"]
         with _ctx(R):
             if s["ev_done"] is not None:
-                R.wait_event(s["ev_done"])   # the set's previous step has finished
+                R.wait_event(s["ev_done"])   # the set's previous step has unpacked
             self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]), sp(R))
             if self.exchange:
                 self._a2a(s["rcnt"], s["scnt"], self.pg_req)
                 self._a2a(s["recv"], s["send"], self.pg_req)
-            if self.cuda:
-                s["ev_req"] = torch.cuda.Event()
-                s["ev_req"].record(R)
-        recv = s["recv"] if self.exchange else s["send"]
-        rcnt = s["rcnt"] if self.exchange else s["scnt"]
-        with _ctx(S):
-            if S is not None:
-                S.wait_event(s["ev_req"])
-                if self.ev_last_merge is not None:
-                    S.wait_event(self.ev_last_merge)
-            self.ops.merge(p(recv), p(rcnt), p(s["order"]), p(s["sms"]), p(s["count"]), sp(S))
-            if S is not None:
-                self.ev_last_merge = torch.cuda.Event()
-                self.ev_last_merge.record(S)
-            self.decide(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(S))
+            self.ops.merge(p(recv), p(rcnt), p(s["order"]), p(s["sms"]), p(s["count"]), sp(R))
+            # the engine's grouping waits for R; U waits for its results
+            self.decide(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(R), sp(U))
+        with _ctx(U):
             if self.exchange:
                 self._a2a(s["back"], s["res"], self.pg_res)
             self.ops.unpack(m, p(s["slot"]), p(s["back"] if self.exchange else s["res"]), p(dec), p(rem), p(retry),
-                            p(reset), sp(S))
-            if S is not None:
+                            p(reset), sp(U))
+            if U is not None:
                 s["ev_done"] = torch.cuda.Event()
-                s["ev_done"].record(S)
-        return S
+                s["ev_done"].record(U)
+        return U
 
     def run(self, batches, outs, done=None):
         """all batches through the pipeline: batches[b] = (key, ts, n, cfg),

@@ -143,6 +143,12 @@ int rl_route_merge(rl_router* r, const rl_route_rec* recv, const int64_t* recv_i
  * waits for `stream` (the merge); `stream` waits for the results. */
 int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
                             const uint32_t* order, const int64_t* server_ms, rl_route_res* res, void* stream);
+/* the same with the two sides on two streams: the grouping waits for
+ * in_stream (the merge), out_stream waits for the results -- so in_stream
+ * can go on with the next step's pack and merge while this one decides */
+int rl_decide_routed_device_io(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
+                               const uint32_t* order, const int64_t* server_ms, rl_route_res* res, void* in_stream,
+                               void* out_stream);
 
 /* sender: back[world * cap] (the result buckets, send layout) -> the caller's
  * order; a dropped request gets decision RL_DROPPED and zeros */

@@ -98,7 +98,7 @@ class NumpyRouteOps:
 def oracle_decide(sim, world, cap):
     """the owner's engine (rl_decide_routed_device) over host pointers,
     backed by the CPU oracle: request p is recv[order[p]], p < count"""
-    def decide(m_max, count, recv, order, sms, res, stream):
+    def decide(m_max, count, recv, order, sms, res, stream, out_stream=None):
         cnt = int(_arr(count, 1, np.int32)[0])
         if cnt == 0:
             return
