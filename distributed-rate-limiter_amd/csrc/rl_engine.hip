@@ -141,7 +141,7 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     const uint32_t* __restrict__ cfg, const CfgDev* __restrict__ cfgs, uint32_t ncfg, TbEntry* tb,
     uint64_t tb_mask, WinEntry* win, uint64_t win_mask, uint32_t win_base, uint32_t invalid_key,
     uint32_t* __restrict__ sk, uint32_t* ghist, int passes, uint32_t shifts, ReqArgs a,
-    ReqRec<XS>* __restrict__ rec, uint32_t* eflags, RouteIn ri, uint32_t* head, uint32_t nhead) {
+    ReqRec<XS>* __restrict__ rec, uint32_t* eflags, RouteIn ri, uint32_t* head, uint32_t nhead, RecSide side) {
     static_assert(!RT || XS, "a routed batch carries its store clock");
     // the batch set's head words (rl_engine.hip CTRL_HEAD), before any later
     // kernel of the batch touches them
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
             // REC_FRESH: this request inserted its key, so no earlier batch
             // has it, and a request alone with its key in the batch starts
             // from the absent state (replay phase 3 then skips the entry read)
-            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r], i | (ins ? REC_FRESH : 0u));
+            rec[i] = rec_pack<XS>(t[r], nn[r], sms[r], c[r], i | (ins ? REC_FRESH : 0u), side);
             for (int p = 0; p < passes; p++)
                 atomicAdd(&lh[p][(slot >> ((shifts >> (8 * p)) & 31u)) & (RADIX - 1)], 1u);
         }
@@ -503,7 +503,11 @@ struct BatchSet {
     int64_t *p_ts = nullptr, *p_n = nullptr, *p_sms = nullptr;
     uint32_t* p_cfg = nullptr;
     void* rec = nullptr;          // requests packed in arrival order (k_probe -> k_permute): ReqRec<XS>
-    void* recb = nullptr;         // ReqRec<false> in the MSD pass's bucket order (k_sort_pass -> k_permute)
+    void* recb = nullptr;         // ReqRec in the MSD pass's bucket order (k_sort_pass -> k_permute)
+    // an explicit server clock's record fields that do not fit (rec_pack), by arrival index
+    int64_t* side_n = nullptr;
+    uint32_t* side_cfg = nullptr;
+    int64_t* side_sms = nullptr;
     uint8_t* p_fresh = nullptr;   // sorted order: the request inserted its key (k_permute -> replay phase 3)
     uint8_t* o_dec = nullptr;
     double* o_tok = nullptr;      // tokens (token bucket) / Remaining bits (window): finish_result
@@ -644,6 +648,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.p_ts); (void)hipFree(B.p_n); (void)hipFree(B.p_sms); (void)hipFree(B.p_cfg);
     (void)hipFree(B.rec);
     (void)hipFree(B.recb);
+    (void)hipFree(B.side_n); (void)hipFree(B.side_cfg); (void)hipFree(B.side_sms);
     (void)hipFree(B.p_fresh);
     (void)hipFree(B.o_dec);
     (void)hipFree(B.o_tok);
@@ -671,7 +676,10 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.p_n, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.p_cfg, 4 * M) == hipSuccess;
-    ok &= hipMalloc(&B.rec, sizeof(ReqRec<true>) * M) == hipSuccess;
+    ok &= hipMalloc(&B.rec, sizeof(ReqRec<false>) * M) == hipSuccess;
+    ok &= hipMalloc(&B.side_n, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.side_cfg, 4 * M) == hipSuccess;
+    ok &= hipMalloc(&B.side_sms, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.recb, sizeof(ReqRec<false>) * M) == hipSuccess;
     ok &= hipMalloc(&B.p_fresh, M) == hipSuccess;
     ok &= hipMalloc(&B.o_dec, M) == hipSuccess;
@@ -1025,21 +1033,24 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     const bool pred_local = e->sort_passes > 1 && (m <= LOC_MAX || *(volatile uint32_t*)e->h_plan == 1u);
     const int hist_passes = pred_local ? 1 : e->sort_passes;
     const RouteIn rin = ri ? *ri : RouteIn{};
+    // an explicit server clock: fields that do not fit the 16-byte record
+    // go to the set's side arrays (rec_pack)
+    const RecSide side{B.side_n, B.side_cfg, B.side_sms};
     if (ri)
         k_probe<1, true, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD);
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD, side);
     else if (xs)
         k_probe<1, true><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD);
+            static_cast<ReqRec<true>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD, side);
     else
         k_probe<1, false><<<probe_grid, PROBE_BLOCK, 0, f>>>(
             m, a.key, a.n, a.cfg, e->d_cfg, (uint32_t)e->h_cfg.size(), e->d_tb, e->tb_cap - 1, e->d_win,
             e->win_cap - 1, e->win_base, e->invalid_key, B.sk0, ghist, hist_passes, e->sort_shifts, a,
-            static_cast<ReqRec<false>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD);
+            static_cast<ReqRec<false>*>(B.rec), e->d_eflags, rin, B.ctrl, CTRL_HEAD, side);
     if (tall) (void)hipEventRecord(ev[1], f);
     uint32_t tiles = (m + SORT_TILE - 1) / SORT_TILE;
     uint32_t *kin = B.sk0, *vin = B.sv0, *kout = B.sk1, *vout = B.sv1;
@@ -1048,12 +1059,9 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     const SegLists lists{{B.list[0], B.list[1], B.list[2], B.list[3]}, segctr, B.claim};
     const uint32_t huge_min = std::max(e->huge_min, e->heavy_min);
     // the request records move with the first pass into its bucket order,
-    // where k_permute gathers them (ReqRec: 16 bytes, 32 with a server clock)
-    // (the 32-byte records of an explicit server clock stay in arrival order:
-    // moving them cost the MSD pass more than the permute's gather saves,
-    // 170-250 against 160 us per routed 1M batch, profiles/r4r_rt_prof)
-    const uint4* rec_in = xs ? nullptr : static_cast<const uint4*>(B.rec);
-    uint4* rec_out = xs ? nullptr : static_cast<uint4*>(B.recb);
+    // where k_permute gathers them (ReqRec, 16 bytes)
+    const uint4* rec_in = static_cast<const uint4*>(B.rec);
+    uint4* rec_out = static_cast<uint4*>(B.recb);
     const int rw = 1;
     if (P <= 1) {
         k_sort_pass<true><<<tiles, SORT_BLOCK, 0, f>>>(kin, vin, kout, vout, m, 0, ghist, B.status,
@@ -1122,13 +1130,13 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     if (xs)
         hipExtLaunchKernelGGL(k_permute<true>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
-                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.rec), a.n, ps, pre, mdev,
-                              a.cfg, vfin);
+                              e->d_cfg, e->profile, static_cast<const ReqRec<true>*>(B.recb), B.side_n, ps, pre,
+                              mdev, B.side_cfg, vfin, (const int64_t*)B.side_sms);
     else
         hipExtLaunchKernelGGL(k_permute<false>, dim3(pgrid_r), dim3(256), (uint32_t)GROUP_LDS, f, nullptr,
                               bind_front ? B.front_done : nullptr, 0u, kin, vin, m, e->invalid_key, e->win_base,
                               e->d_cfg, e->profile, static_cast<const ReqRec<false>*>(B.recb), a.n, ps, pre, mdev,
-                              a.cfg, vfin);
+                              a.cfg, vfin, (const int64_t*)nullptr);
     if (tall) (void)hipEventRecord(ev[3], f);
     if (sr) k_stamp<<<1, 64, 0, f>>>(sr + 1);
     if (!bind_front) HIPCHK(e, hipEventRecord(B.front_done, f));

@@ -997,66 +997,66 @@ __global__ __launch_bounds__(LOC_BLOCK) void k_sort_local(const uint32_t* kin, c
 }
 
 // One request as k_probe packs it in arrival order: the sorted-order gather
-// of k_permute reads one record per request instead of four scattered array
-// elements.  Without an explicit server clock (XS false, the common case) the
-// record is 16 bytes -- time, config and n when it fits 32 bits (a larger n
-// is read from the caller's array) -- and the clock is floor(ts / 1e6); with
-// one (XS, the routed path's store clock) it is 32 bytes.  Either carries its
-// arrival index, because the grouping sort's first (MSD) pass moves it into
-// bucket order (k_sort_pass rin/rout), where k_permute gathers it from an
-// L2-resident bucket instead of from the whole batch.
-template <bool XS> struct ReqRec;
-// 16 bytes: config and n take 16 bits each (REC_WIDE: read the caller's array
-// at the arrival index)
-template <> struct alignas(16) ReqRec<false> {
+// of k_permute reads one 16-byte record per request instead of four scattered
+// array elements -- time, arrival index, config and n in 16 bits each.  The
+// grouping sort's first (MSD) pass moves it into bucket order (k_sort_pass
+// rin/rout), where k_permute gathers it from an L2-resident bucket instead of
+// from the whole batch.  A field that does not fit (REC_WIDE) is read at the
+// arrival index from the caller's arrays, or, with an explicit server clock
+// (XS: the routed path's store clock), from side arrays the probe filled for
+// exactly those requests; the clock itself is floor(ts / 1e6) unless
+// REC_SMSX says it differs (XS: then side.sms at the arrival index).
+template <bool XS> struct alignas(16) ReqRec {
     int64_t ts;
-    uint32_t ix;       // arrival index
+    uint32_t ix;       // arrival index | REC_FRESH | REC_SMSX
     uint32_t cn;       // config id << 16 | n
 };
-template <> struct alignas(32) ReqRec<true> {
-    int64_t ts, n, sms;
-    uint32_t cfg;
-    uint32_t ix;       // arrival index
-};
-constexpr uint32_t REC_WIDE = 0xffffu;   // a 16-bit field that does not fit
+constexpr uint32_t REC_WIDE = 0xffffu;    // a 16-bit field that does not fit
 constexpr uint32_t REC_FRESH = 1u << 31;  // ix: the request's probe inserted its key (k_probe)
-static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 32, "request records");
+constexpr uint32_t REC_SMSX = 1u << 30;   // ix (XS): the server clock is not floor(ts / 1e6)
+constexpr uint32_t REC_IX = REC_SMSX - 1u;
+static_assert(sizeof(ReqRec<false>) == 16 && sizeof(ReqRec<true>) == 16, "request records");
+
+// where an XS record's fields that do not fit go (arrival index)
+struct RecSide {
+    int64_t* n;
+    uint32_t* cfg;
+    int64_t* sms;
+};
 
 template <bool XS>
-__device__ inline ReqRec<XS> rec_pack(int64_t t, int64_t n, int64_t sms, uint32_t c, uint32_t i) {
+__device__ inline ReqRec<XS> rec_pack(int64_t t, int64_t n, int64_t sms, uint32_t c, uint32_t i, const RecSide& side) {
+    const uint32_t c16 = c < REC_WIDE ? c : REC_WIDE;
+    const uint32_t n16 = (n > 0 && n < (int64_t)REC_WIDE) ? (uint32_t)n : REC_WIDE;
+    uint32_t ix = i;
     if constexpr (XS) {
-        return ReqRec<true>{t, n, sms, c, i};
+        const uint32_t a = i & REC_IX;
+        if (c16 == REC_WIDE) side.cfg[a] = c;
+        if (n16 == REC_WIDE) side.n[a] = n;
+        if (sms != floor_div(t, 1000000LL)) {
+            side.sms[a] = sms;
+            ix |= REC_SMSX;
+        }
     } else {
         (void)sms;
-        const uint32_t c16 = c < REC_WIDE ? c : REC_WIDE;
-        const uint32_t n16 = (n > 0 && n < (int64_t)REC_WIDE) ? (uint32_t)n : REC_WIDE;
-        return ReqRec<false>{t, i, (c16 << 16) | n16};
+        (void)side;
     }
+    return ReqRec<XS>{t, ix, (c16 << 16) | n16};
 }
 template <bool XS>
 __device__ inline int64_t rec_n(const ReqRec<XS>& r, const int64_t* __restrict__ n_in, uint32_t i) {
-    if constexpr (XS) {
-        (void)n_in; (void)i;
-        return r.n;
-    } else {
-        const uint32_t n16 = r.cn & 0xffffu;
-        return n16 != REC_WIDE ? (int64_t)n16 : n_in[i];
-    }
+    const uint32_t n16 = r.cn & 0xffffu;
+    return n16 != REC_WIDE ? (int64_t)n16 : n_in[i];
 }
 template <bool XS>
 __device__ inline uint32_t rec_cfg(const ReqRec<XS>& r, const uint32_t* __restrict__ cfg_in, uint32_t i) {
-    if constexpr (XS) {
-        (void)cfg_in; (void)i;
-        return r.cfg;
-    } else {
-        const uint32_t c16 = r.cn >> 16;
-        return c16 != REC_WIDE ? c16 : cfg_in[i];
-    }
+    const uint32_t c16 = r.cn >> 16;
+    return c16 != REC_WIDE ? c16 : cfg_in[i];
 }
 template <bool XS>
-__device__ inline int64_t rec_sms(const ReqRec<XS>& r) {
-    if constexpr (XS) return r.sms;
-    else return floor_div(r.ts, 1000000LL);
+__device__ inline int64_t rec_sms(const ReqRec<XS>& r, const int64_t* __restrict__ sms_in) {
+    if (XS && (r.ix & REC_SMSX)) return sms_in[r.ix & REC_IX];
+    return floor_div(r.ts, 1000000LL);
 }
 
 // requests to sorted order + the state-free token-bucket precomputation.
@@ -1075,7 +1075,8 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
                                                  const CfgDev* __restrict__ cfgs, int32_t profile,
                                                  const ReqRec<XS>* __restrict__ rec, const int64_t* __restrict__ n_in,
                                                  ReqArgs out, TbPre pre, const uint32_t* mdev,
-                                                 const uint32_t* __restrict__ cfg_in, uint32_t* __restrict__ ix_out) {
+                                                 const uint32_t* __restrict__ cfg_in, uint32_t* __restrict__ ix_out,
+                                                 const int64_t* __restrict__ sms_in) {
     if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -1094,13 +1095,13 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
         ReqRec<XS> r{}, q{};
         if (j < m) r = rec[at];
         if (lane == 0 && kpl == k0 && k0 != invalid_key) q = rec[atp];
-        const uint32_t ix = r.ix & ~REC_FRESH;
+        const uint32_t ix = r.ix & REC_IX;
         if (j < m) {
             ix_out[j] = ix;
             if (out.fresh) const_cast<uint8_t*>(out.fresh)[j] = (uint8_t)(r.ix >> 31);
         }
         const bool valid = k0 != invalid_key;
-        const int64_t sms = rec_sms<XS>(r);
+        const int64_t sms = rec_sms<XS>(r, sms_in);
         // predecessor (j-1) fields from the lane below
         const uint32_t rc = valid ? rec_cfg<XS>(r, cfg_in, ix) : 0u;
         uint32_t kp = __shfl_up(k0, 1);
@@ -1112,8 +1113,8 @@ __global__ __launch_bounds__(256) void k_permute(const uint32_t* __restrict__ sk
             if (kpl == k0 && valid) {
                 kp = k0;
                 tp = q.ts;
-                smsp = rec_sms<XS>(q);
-                cp = rec_cfg<XS>(q, cfg_in, q.ix & ~REC_FRESH);
+                smsp = rec_sms<XS>(q, sms_in);
+                cp = rec_cfg<XS>(q, cfg_in, q.ix & REC_IX);
             }
         }
         if (!valid) continue;
