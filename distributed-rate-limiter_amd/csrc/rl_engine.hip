@@ -426,6 +426,41 @@ __global__ __launch_bounds__(256) void k_unpermute_routed(const uint32_t* __rest
     }
 }
 
+// the same through merge-position buckets (m <= UP_MAX): k_unpermute_bucket
+// has placed each request's decision and value in the bucket of its merge
+// position p; one block per bucket finishes the Result fields in p order from
+// the request's record and writes the result records at p (identity) or
+// order[p]
+__global__ __launch_bounds__(256) void k_unpermute_routed_out(uint32_t m, const UpRec* __restrict__ bucketed,
+                                                              const CfgDev* __restrict__ cfgs, RouteIn ri) {
+    __shared__ double s_val[UP_BUCKET];
+    __shared__ uint8_t s_dec[UP_BUCKET];
+    m = min(m, *ri.count);
+    const uint32_t base = blockIdx.x * UP_BUCKET;
+    if (base >= m) return;   // block-uniform
+    const bool ident = ri.order[0] == RL_ORDER_IDENTITY;
+    const uint32_t cnt = min(UP_BUCKET, m - base);
+    for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
+        const UpRec r = bucketed[(size_t)base + k];
+        const uint32_t o = r.i - base;
+        s_dec[o] = (uint8_t)r.dec;
+        s_val[o] = r.val;
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < cnt; k += 256) {
+        const uint32_t p = base + k;
+        const uint32_t at = ident ? p : ri.order[p];
+        const uint8_t dec = s_dec[k];
+        int64_t rem = 0, retry = 0, reset = 0;
+        double tok = 0.0;
+        if (dec != DEC_INVALID) {
+            const rl_route_rec q = ri.rec[at];
+            finish_result(dec, s_val[k], q.ts, q.n, cfgs[q.cfg], rem, retry, reset, tok);
+        }
+        ri.res[at] = rl_route_res{(int64_t)dec, rem, retry, reset};
+    }
+}
+
 // diagnostic timestamp (10 ns ticks) into *w
 __global__ void k_stamp(uint32_t* w) { *w = (uint32_t)__builtin_amdgcn_s_memrealtime(); }
 
@@ -1188,10 +1223,15 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
     if (ri) {
-        // a routed batch: one result record per request at its receive index
-        // (measured: through merge-position buckets as below it took 107 us
-        // per 1M-request step against this kernel's 64)
-        k_unpermute_routed<<<pgrid, 256, GROUP_LDS, t>>>(kin, vfin, m, e->invalid_key, e->d_cfg, ps, *ri);
+        // a routed batch: one result record per request at its receive
+        // index, through merge-position buckets (no scattered 32-byte stores:
+        // routed mixed +3.5 %, profiles/r4w_ab_routed_finish.txt)
+        if (m <= UP_MAX) {
+            k_unpermute_bucket<<<(m + 256 * UP_ITEMS - 1) / (256 * UP_ITEMS), 256, GROUP_LDS, t>>>(
+                kin, vfin, m, e->invalid_key, ps, B.upb, B.ctrl + CTRL_UPB, ri->count);
+            k_unpermute_routed_out<<<(m + UP_BUCKET - 1) / UP_BUCKET, 256, 0, t>>>(m, B.upb, e->d_cfg, *ri);
+        } else
+            k_unpermute_routed<<<pgrid, 256, GROUP_LDS, t>>>(kin, vfin, m, e->invalid_key, e->d_cfg, ps, *ri);
     } else if (m <= UP_MAX) {
         // results to the caller's order through arrival-index buckets: no
         // scattered partial-line stores

@@ -1218,7 +1218,7 @@ __global__ __launch_bounds__(256) void k_unpermute(const uint32_t* __restrict__ 
 // writes every output array with full-line stores.
 constexpr int UP_BUCKET_BITS = 11;
 constexpr uint32_t UP_BUCKET = 1u << UP_BUCKET_BITS;   // arrival indices per bucket
-constexpr uint32_t UP_MAX = 1u << 20;                  // batches up to 2^20: <= 512 buckets
+constexpr uint32_t UP_MAX = 1u << 21;                  // batches up to 2^21: <= 1024 buckets
 constexpr uint32_t UP_NB = UP_MAX / UP_BUCKET;
 constexpr int UP_ITEMS = 8;                            // sorted positions per thread (k_unpermute_bucket)
 
@@ -1231,8 +1231,10 @@ struct alignas(16) UpRec {
 __global__ __launch_bounds__(256) void k_unpermute_bucket(const uint32_t* __restrict__ sk,
                                                           const uint32_t* __restrict__ sv, uint32_t m,
                                                           uint32_t invalid_key, ReqArgs sorted,
-                                                          UpRec* __restrict__ bucketed, uint32_t* bucket_ctr) {
+                                                          UpRec* __restrict__ bucketed, uint32_t* bucket_ctr,
+                                                          const uint32_t* mdev = nullptr) {
     __shared__ uint32_t s_cnt[UP_NB], s_base[UP_NB];
+    if (mdev) m = min(m, *mdev);   // a batch sized on the device (routed)
     const uint32_t nb = (m + UP_BUCKET - 1) >> UP_BUCKET_BITS;
     for (uint32_t b = threadIdx.x; b < nb; b += 256) s_cnt[b] = 0;
     __syncthreads();
