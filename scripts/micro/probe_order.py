@@ -5,7 +5,10 @@ engine with per-stage timing, twice: batches as generated (arrival order:
 random table lines) and with each batch's keys reordered by home slot (the
 table line the probe reads first), timestamps kept in place.  The second is
 not the reference's semantics (it moves requests in time); it only measures
-the stage times of a home-ordered probe.  Prints one JSON line per order."""
+the stage times of a home-ordered probe.  A third order ("xcd") puts each
+key where a block of the XCD that owns its table eighth probes it (blocks
+are dealt round-robin over the 8 XCDs), to measure per-XCD slicing of the
+table instead of a full sort.  Prints one JSON line per order."""
 import json
 import os
 import sys
@@ -37,7 +40,29 @@ def main():
     gen = traces.MixedTenants(batch=m)
     batches = [gen.next_batch() for _ in range(nb)]
     dev = torch.device("cuda:0")
-    for order in ("arrival", "home"):
+    def xcd_order(key, cfg):
+        # positions i with (i // 256) % 8 == s get keys whose home slot lies in
+        # eighth s of its table: k_probe's block b (256 requests per grid step)
+        # then touches one eighth of each table, and blocks b, b + 8, ... share
+        # an XCD (round-robin placement), so each XCD touches one eighth
+        home = mix64(key) & np.uint64(cap - 1)
+        sl = (home >> np.uint64(23)).astype(np.int64)          # 2^26 / 8 = 2^23
+        want = (np.arange(key.size) // 256) % 8
+        o = np.empty(key.size, np.int64)
+        pools = [list(np.nonzero(sl == x)[0]) for x in range(8)]
+        ptr = [0] * 8
+        rest = []
+        pos_by = [np.nonzero(want == x)[0] for x in range(8)]
+        for x in range(8):
+            k = min(len(pools[x]), len(pos_by[x]))
+            o[pos_by[x][:k]] = pools[x][:k]
+            rest += list(pools[x][k:])
+            ptr[x] = k
+        free = np.concatenate([pos_by[x][ptr[x]:] for x in range(8)])
+        o[np.sort(free)] = np.array(rest, np.int64)
+        return o
+
+    for order in ("arrival", "home", "xcd"):
         eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=cap, win_capacity=cap, max_batch=m,
                             device=0, flags=rl_amd.OPT_PIPELINE)
         for a, L, W in gen.configs:
@@ -45,6 +70,9 @@ def main():
         algs = np.array([a for a, _, _ in gen.configs])
         dbs = []
         for key, ts, n, cfg in batches:
+            if order == "xcd":
+                o = xcd_order(key, cfg)
+                key, cfg, n = key[o], cfg[o], n[o]
             if order == "home":
                 table = (algs[cfg] != 1).astype(np.uint64)     # 1: token bucket table, else window table
                 home = (table << np.uint64(40)) | (mix64(key) & np.uint64(cap - 1))
