@@ -88,6 +88,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     if (mdev) m = min(m, *mdev);   // a batch sized on the device (the routed path): m is its bound
     __shared__ uint32_t s_wcnt[SORT_WAVES][RADIX];
     __shared__ uint32_t s_goff[RADIX];
+    __shared__ uint32_t s_tstart[RADIX];
+    __shared__ uint32_t s_key[SORT_TILE], s_src[SORT_TILE];
     __shared__ uint32_t s_tmp[SORT_WAVES];
     __shared__ uint32_t s_tile;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -179,23 +181,40 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_pass(
     }
     uint32_t g = block_excl_scan_256(gh, s_tmp);
     s_goff[tid] = g + excl;
+    __syncthreads();   // s_tmp is reused by the next scan
+    s_tstart[tid] = block_excl_scan_256(tot, s_tmp);   // the digit's first position in the tile
     __syncthreads();
+    // the tile in output order in LDS, then written out with consecutive
+    // threads on consecutive positions of each digit's run: every run of a
+    // bucket is one stretch of full lines instead of one scattered element
+    // per lane (and records are read from the tile's L2-resident input range)
 #pragma unroll
     for (int j = 0; j < SORT_ITEMS; j++) {
         uint32_t idx = base + j * 64 + lane;
         if (idx < m) {
             uint32_t d = (key[j] >> shift) & (RADIX - 1);
-            uint32_t pos = s_goff[d] + s_wcnt[wave][d] + rank[j];
-            kout[pos] = key[j];
-            if (FIRST && rout) {
-                vout[pos] = pos;
-                for (int w = 0; w < rw; w++) rout[(size_t)pos * rw + w] = rin[(size_t)idx * rw + w];
-            } else {
-                vout[pos] = val[j];
-            }
+            uint32_t li = s_tstart[d] + s_wcnt[wave][d] + rank[j];
+            s_key[li] = key[j];
+            s_src[li] = FIRST ? idx : val[j];
         }
     }
-    __syncthreads();   // s_tile, s_wcnt, s_goff, s_tmp are rewritten by the next tile
+    __syncthreads();
+    const uint32_t t0 = tile * SORT_TILE;
+    const uint32_t nt = m - t0 < (uint32_t)SORT_TILE ? m - t0 : (uint32_t)SORT_TILE;
+    for (uint32_t t = tid; t < nt; t += SORT_BLOCK) {
+        const uint32_t k = s_key[t];
+        const uint32_t d = (k >> shift) & (RADIX - 1);
+        const uint32_t pos = s_goff[d] + (t - s_tstart[d]);
+        const uint32_t src = s_src[t];
+        kout[pos] = k;
+        if (FIRST && rout) {
+            vout[pos] = pos;
+            for (int w = 0; w < rw; w++) rout[(size_t)pos * rw + w] = rin[(size_t)src * rw + w];
+        } else {
+            vout[pos] = src;   // FIRST: the input index
+        }
+    }
+    __syncthreads();   // s_tile, s_wcnt, s_goff, s_tstart, s_key, s_src, s_tmp are rewritten by the next tile
     }
 }
 
