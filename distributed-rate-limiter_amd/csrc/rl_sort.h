@@ -8,7 +8,8 @@
 //     (8 ballots per element match the 8-bit digit across the 64 lanes, LDS
 //     digit counters per wave, 2 barriers per tile), the tile's per-digit
 //     offsets come from a decoupled look-back over earlier tiles, then keys and
-//     values are scattered.
+//     values are staged in LDS in output order (digit-major) and written by
+//     consecutive threads, so each digit's run leaves as full-line stores.
 // Look-back words pack {2-bit flag, 30-bit count} in one 32-bit word, stored
 // and loaded with relaxed agent-scope atomics (global_store/load sc1): the
 // word is its own granule, so no fence is needed (MI355X_MICROARCH.md,
