@@ -80,6 +80,53 @@ def test_route_pack_matches_restatement(rl, world, cap):
     r.close()
 
 
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_route_pack_repeated_calls(rl, world):
+    """one router, many packs of varying sizes (empty, under one tile, ragged,
+    many tiles, sorted and unsorted): the one-pass pack's look-back words and
+    accumulators carry nothing from one call to the next"""
+    import torch
+
+    import route_ops
+    rng = np.random.default_rng(77 + world)
+    M = 50_000
+    cap = 12_000
+    r = rl.Router(0, world, M, cap)
+    C = r.capacity
+    s = torch.cuda.current_stream().cuda_stream
+    for m in [5000, 0, 1, 1023, 1024, 1025, M, 3, 40_000, 777, M]:
+        ops = route_ops.NumpyRouteOps(world, cap)
+        key = rng.integers(0, 1 << 63, m).astype(np.uint64)
+        ts = T0 + rng.integers(0, 2_000_000_000, m).astype(np.int64)
+        if m % 2:
+            ts.sort()
+        n = rng.integers(1, 9, m).astype(np.int64)
+        cfg = rng.integers(0, 15, m).astype(np.uint32)
+        k, t, nn, c = _dev_tensors(torch, key, ts, n, cfg) if m else [torch.empty(1, dtype=torch.int64,
+                                                                                  device="cuda")] * 4
+        send = torch.empty((world * C, 4), dtype=torch.int64, device="cuda")
+        scnt = torch.full((world, 4), -7, dtype=torch.int64, device="cuda")
+        slot = torch.empty(max(m, 1), dtype=torch.int32, device="cuda")
+        r.pack(m, k.data_ptr(), t.data_ptr(), nn.data_ptr(), c.data_ptr(), send.data_ptr(), scnt.data_ptr(),
+               slot.data_ptr(), s)
+        kc, tc, nc, cc = _host(torch, key, ts, n, cfg)
+        send_h = torch.zeros((world * C, 4), dtype=torch.int64)
+        scnt_h = torch.empty((world, 4), dtype=torch.int64)
+        slot_h = torch.empty(max(m, 1), dtype=torch.int32)
+        ops.pack(m, kc.data_ptr(), tc.data_ptr(), nc.data_ptr(), cc.data_ptr(), send_h.data_ptr(),
+                 scnt_h.data_ptr(), slot_h.data_ptr(), None)
+        torch.cuda.synchronize()
+        assert torch.equal(scnt.cpu(), scnt_h), m
+        assert torch.equal(slot.cpu()[:m], slot_h[:m]), m
+        sd = send.cpu()
+        for o in range(world):
+            c_o = int(scnt_h[o, 0])
+            assert torch.equal(sd[o * C:o * C + c_o], send_h[o * C:o * C + c_o]), (m, o)
+        dropped = int((scnt_h[:, 3] >> 1).sum())
+        assert r.sync(s) == (rl.RL_EOVERFLOW if dropped else rl.RL_OK), m
+    r.close()
+
+
 def _merge_case(rng, world, C, counts, span, step_base):
     """received buckets: source q's counts[q] records, times out of order in
     the even sources (flagged in the info row) and sorted in the odd ones,
