@@ -242,6 +242,9 @@ KEYSPACE = {"tb_zipf": (1 << 21, 1024), "tb_zipf15": (1 << 21, 1024), "tb_hot": 
             "fw_uniform": (1024, 1 << 15), "sw_bursty": (1024, 1 << 27), "mixed": (1 << 26, 1 << 26)}
 
 
+REPLAY_EVENT_STRIDE = 2   # replay timing events on every 2nd launch of the timed region
+
+
 def roofline_of(replay_ms, algs, uniq, m, workload):
     """the dominant kernel is the replay (k_tb_chain: every decision's script
     replay, the path's critical kernel); its launch time comes from HIP events
@@ -349,9 +352,11 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     rc = eng.sync()
     if rc != 0:
         raise SystemExit(f"engine error during warmup: {rc} {eng.last_error()}")
-    # timed region: events around the replay only (two per batch on its
-    # stream); the per-stage breakdown comes from the latency phase below
-    timing = 0 if os.environ.get("RL_BENCH_NO_TIMING") else 1
+    # timed region: events around the replay only, on every 2nd launch (two
+    # per sampled batch on its stream: each pair costs the replay stream
+    # ~10 us, profiles/r4tm_timing_events.txt); the per-stage breakdown comes
+    # from the latency phase below
+    timing = 0 if os.environ.get("RL_BENCH_NO_TIMING") else -REPLAY_EVENT_STRIDE
     eng.set_timing(timing)
     eng.stage_times()  # clear
 
@@ -370,6 +375,7 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
         raise SystemExit(f"engine error during timed region: {rc} {eng.last_error()}")
     stage_ms, nbat = eng.stage_times()
     replay_ms = stage_ms[3] / nbat if timing else float("nan")
+    replay_timed = int(nbat)
     st = eng.stats()
     dbgw = eng.debug_words()
     stamp_ring = None
@@ -420,6 +426,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     roof, per_launch_ms = roofline_of(replay_ms, algs, uniq, m, workload)
+    roof["launches_timed"] = replay_timed
+    roof["launch_ms_how"] = (f"HIP events on the replay's dispatch packets, every {REPLAY_EVENT_STRIDE}nd launch "
+                             f"of the timed region")
     latency = None
     if lat:
         la = np.array(lat) * 1e3
@@ -506,7 +515,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         if rc != 0:
             raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}"
                              + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
-    eng.set_timing(0 if os.environ.get("RL_BENCH_NO_TIMING") else 1)
+    eng.set_timing(0 if os.environ.get("RL_BENCH_NO_TIMING") else -REPLAY_EVENT_STRIDE)
     eng.stage_times()
     dist.barrier()
     torch.cuda.synchronize()

@@ -642,6 +642,8 @@ struct rl_engine {
     // (front); replay start, end (chain); finish start, end (tail)
     bool timing = false;
     bool timing_all = false;    // level 2: every stage; level 1: the replay only (2 events per batch)
+    uint32_t timing_stride = 1; // the replay events on every timing_stride-th batch only (level -k)
+    uint64_t timing_seq = 0;
     bool stamps = false;        // RL_STAMP_KERNELS: timestamps around each replay (debug words 18, 19)
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::array<hipEvent_t, 8>> ev_pending;
@@ -1046,8 +1048,11 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         a.key = B.kid;
     }
     std::array<hipEvent_t, 8> ev{};
-    const bool tall = e->timing && e->timing_all;   // stage events on every stream
-    if (e->timing) {
+    // this batch carries timing events (every timing_stride-th batch: each
+    // event pair on the replay's dispatch costs the chain stream ~10 us)
+    const bool timed = e->timing && (e->timing_stride <= 1 || e->timing_seq++ % e->timing_stride == 0);
+    const bool tall = timed && e->timing_all;   // stage events on every stream
+    if (timed) {
         for (int k = 0; k < 8; k++)
             if (tall || k == 4 || k == 5) ev[k] = take_event(e);
         if (tall) (void)hipEventRecord(ev[0], f);
@@ -1183,14 +1188,14 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // replay timing: the two events ride on the replay's own dispatch packet
     // (hipExtLaunchKernel) instead of two marker packets around it, unless
     // the stamp kernels must sit inside the timed interval
-    const bool bound_ev = e->timing && !e->stamps && !sr;
-    if (e->timing && !bound_ev) (void)hipEventRecord(ev[4], c);
+    const bool bound_ev = timed && !e->stamps && !sr;
+    if (timed && !bound_ev) (void)hipEventRecord(ev[4], c);
     if (e->stamps) k_stamp<<<1, 64, 0, c>>>(B.ctrl + CTRL_DBG + 18);
     if (sr) k_stamp<<<1, 64, 0, c>>>(sr + 2);
     const uint32_t ncfg = (uint32_t)e->h_cfg.size();
     uint32_t* dbg = B.ctrl + CTRL_DBG;
     // timing off: chain_done rides on the dispatch instead
-    const bool bind_done = !e->timing && !e->stamps && !sr;
+    const bool bind_done = !timed && !e->stamps && !sr;
     const hipEvent_t ev_a = bound_ev ? ev[4] : nullptr, ev_b = bound_ev ? ev[5] : bind_done ? B.chain_done : nullptr;
     if (ncfg <= (uint32_t)MAX_LCFG)
         hipExtLaunchKernelGGL(k_tb_chain<true>, dim3(e->coop_grid), dim3(CH_BLOCK), (uint32_t)e->chain_pad[0], c, ev_a, ev_b,
@@ -1210,7 +1215,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     hipEvent_t chain_end = B.chain_done;
     if (bound_ev) {
         chain_end = ev[5];
-    } else if (e->timing) {
+    } else if (timed) {
         HIPCHK(e, hipEventRecord(ev[5], c));
         chain_end = ev[5];
     } else if (!bind_done) {
@@ -1242,7 +1247,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
         k_unpermute<<<pgrid, 256, GROUP_LDS, t>>>(kin, vfin, m, e->invalid_key, e->d_cfg, ps, a);
     }
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 5);
-    if (e->timing) {
+    if (timed) {
         if (tall) (void)hipEventRecord(ev[7], t);
         e->ev_pending.push_back(ev);
     }
@@ -1584,7 +1589,9 @@ extern "C" int rl_engine_stats(rl_engine* e, rl_stats* out) {
 extern "C" int rl_engine_set_timing(rl_engine* e, int on) {
     if (!e) return RL_EINVAL;
     e->timing = on != 0;
-    e->timing_all = on != 1;   // 1: replay events only
+    e->timing_all = on > 1;    // 1 or -k: replay events only
+    e->timing_stride = on < 0 ? (uint32_t)(-(int64_t)on) : 1u;
+    e->timing_seq = 0;
     return RL_OK;
 }
 

@@ -354,7 +354,9 @@ class Engine:
         return rc, out
 
     def set_timing(self, level):
-        """0 off, 1 replay events only (timed runs), 2 every stage (True == 2)"""
+        """0 off, 1 replay events only, 2 every stage (True == 2), -k replay
+        events on every k-th batch only (timed runs: each event pair costs the
+        replay stream ~10 us)"""
         lib.rl_engine_set_timing(self.h, 2 if level is True else int(level))
 
     def stage_times(self):

@@ -198,8 +198,9 @@ int rl_table_gc(rl_engine* e, int64_t now_ms, uint64_t tb_capacity, uint64_t win
  * HIP events on the stream the kernels run on; stages: 0 probe, 1 sort,
  * 2 segments + permute, 3 replay (k_tb_chain), 4 finish (run expansion +
  * unpermute).  rl_engine_set_timing(e, on): 0 off, 1 the replay only (two
- * events per batch on its stream: what a timed benchmark can afford), 2 every
- * stage. */
+ * events per batch on its stream), 2 every stage, -k (k >= 2) the replay
+ * only on every k-th batch (the event pair costs the replay stream ~10 us per
+ * batch; a timed benchmark samples).  *batches counts the batches timed. */
 int rl_engine_set_timing(rl_engine* e, int on);
 int rl_engine_stage_times(rl_engine* e, double* ms, int nstages, uint64_t* batches);
 /* diagnostic: the last batch's replay debug counters (up to 88 words; layout in rl_engine.hip CTRL_DBG) */

@@ -495,12 +495,13 @@ def test_device_api_batches_in_flight(rl, pipeline):
         assert_same(res, ref, configs, cfg, what=f"batch {i}")
 
 
-@pytest.mark.parametrize("level", [1, 2])
+@pytest.mark.parametrize("level", [1, 2, -2])
 def test_timed_pipelined_batches(rl, level):
     """Stage timing on (level 1: the replay's events are bound to its dispatch
     and also order the finish stream; level 2: marker events around every
-    stage) over pipelined hot-key batches: results equal the oracle's and the
-    replay time is reported."""
+    stage; level -2: the replay's events on every 2nd batch, the others bind
+    the plain done event) over pipelined hot-key batches: results equal the
+    oracle's and the replay time is reported for the batches timed."""
     import torch
     g = traces.TokenBucketZipf(batch=100_000)
     eng = rl.Engine(profile=0, tb_capacity=1 << 20, win_capacity=1024, max_batch=1 << 17, flags=rl.OPT_PIPELINE)
@@ -529,7 +530,8 @@ def test_timed_pipelined_batches(rl, level):
     assert eng.sync() == 0, eng.last_error()
     ms, nb = eng.stage_times()
     eng.set_timing(0)
-    assert nb == len(parts) and ms[3] > 0
+    assert nb == (len(parts) + 1) // 2 if level == -2 else len(parts)
+    assert ms[3] > 0
     for i, ((key, ts, n, cfg), o) in enumerate(zip(parts, outs)):
         ref = sim.decide(key, ts, n, cfg)
         res = rl.Decisions(*[x.cpu().numpy() for x in o])
