@@ -489,16 +489,27 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     nb = args.warmup + args.steps
     m = args.batch
     host = [gen.next_batch() for _ in range(nb)]
+    # bucket capacity per peer (every rank the same: the all-to-alls' equal
+    # splits).  A uniform hash partition needs ~m / world plus a margin; a Zipf
+    # hot key lands on one owner (12.4 % of every rank's batch at s = 1.1).
+    # Sized from the trace itself: the largest per-owner count of any rank's
+    # batch, so no request of the run is ever dropped (RL_ROUTE_SLACK = f
+    # sizes f * m / world instead)
+    slack = float(os.environ.get("RL_ROUTE_SLACK", "0"))
+    if world == 1:
+        cap = m
+    elif slack:
+        cap = min(m, int(np.ceil(slack * m / world)))
+    else:
+        need = max(int(np.bincount(shard.owner_of(k, world), minlength=world).max()) for k, _, _, _ in host)
+        need_t = torch.tensor([need], dtype=torch.int64, device=dev)
+        dist.all_reduce(need_t, op=dist.ReduceOp.MAX)
+        cap = min(m, max(int(need_t.item()), int(np.ceil(1.05 * m / world))))
     ins = [(torch.from_numpy(k.view(np.int64)).to(dev), torch.from_numpy(t).to(dev), torch.from_numpy(n).to(dev),
             torch.from_numpy(c.view(np.int32)).to(dev)) for k, t, n, c in host]
     del host
     algs = {a for a, _, _ in gen.configs}
     tb_cap, win_cap = KEYSPACE[workload]
-    # bucket capacity per peer: a uniform hash partition needs ~m / world plus
-    # a margin; a Zipf hot key lands on one owner (12.4 % of every rank's
-    # batch at s = 1.1), so that workload gets twice the share
-    slack = float(os.environ.get("RL_ROUTE_SLACK", "0")) or (2.0 if workload == "tb_zipf" else 1.25)
-    cap = m if world == 1 else min(m, int(np.ceil(slack * m / world)))
     router = rl_amd.Router(local_rank, world, m, cap)
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=tb_cap, win_capacity=win_cap,
                         max_batch=world * router.capacity, device=local_rank, flags=0)
@@ -509,12 +520,21 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
                                 depth=int(os.environ.get("RL_ROUTE_DEPTH", "4")), exchange=exchange)
     outs = [(torch.empty(m, dtype=torch.uint8, device=dev),) +
             tuple(torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)) for _ in range(pipe.depth)]
+    def check(when):
+        # every rank takes the same branch (a rank that stopped alone would
+        # leave the others in a collective): the worst code over the ranks
+        rcs = [eng.sync(), router.sync(None)]
+        t = torch.tensor(rcs, dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        for what, rc, mine in zip(("engine", "router"), t.tolist(), rcs):
+            if rc != 0:
+                raise RuntimeError(f"{what} error during {when}: {rc}"
+                                   + (f" {eng.last_error()}" if mine else " (on another rank)")
+                                   + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
+
     pipe.run(ins[:args.warmup], [outs[b % pipe.depth] for b in range(args.warmup)])
     torch.cuda.synchronize()
-    for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
-        if rc != 0:
-            raise SystemExit(f"{what} error during warmup: {rc} {eng.last_error()}"
-                             + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
+    check("warmup")
     eng.set_timing(0 if os.environ.get("RL_BENCH_NO_TIMING") else -REPLAY_EVENT_STRIDE)
     eng.stage_times()
     dist.barrier()
@@ -525,10 +545,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    for what, rc in (("engine", eng.sync()), ("router", router.sync(None))):
-        if rc != 0:
-            raise SystemExit(f"{what} error during timed region: {rc} {eng.last_error()}"
-                             + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
+    check("timed region")
     stage_ms, nbat = eng.stage_times()
     st = eng.stats()
     eng.set_timing(0)
@@ -548,6 +565,8 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
                     + "; merge and engine sized on the device, no host read in the step (include/rl_route.h)"),
         "batch": m,
         "bucket_capacity": router.capacity,
+        "collective_order": f"one order over both groups, result exchange {pipe.lookahead} step(s) late"
+        if exchange else "none (world 1, buckets read in place)",
         "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
         "roofline": roof,
     }
@@ -640,10 +659,16 @@ def main():
         for wl, ing in (("tb_zipf", "routed"), (workload, "sharded")):
             if (wl, ing) == (workload, ingress):
                 continue
-            r2 = (bench_routed(args, wl, world, rank, local_rank, dev, pg_res) if ing == "routed"
-                  else bench_local(args, wl, world, rank, local_rank, dev, sharded=True))
-            secondary.append({k: r2[k] for k in ("value", "ms_per_step", "workload", "ingress")} |
-                             {"unit": "decisions/s", "roofline_frac": r2["roofline"]["frac"]})
+            # a secondary line that fails is reported inside the line; the
+            # headline stands (the failure is the same on every rank: the
+            # routed checks agree over the ranks before raising)
+            try:
+                r2 = (bench_routed(args, wl, world, rank, local_rank, dev, pg_res) if ing == "routed"
+                      else bench_local(args, wl, world, rank, local_rank, dev, sharded=True))
+                secondary.append({k: r2[k] for k in ("value", "ms_per_step", "workload", "ingress")} |
+                                 {"unit": "decisions/s", "roofline_frac": r2["roofline"]["frac"]})
+            except (Exception, SystemExit) as ex:   # noqa: BLE001
+                secondary.append({"workload": WORKLOAD_DESC.get(wl, wl), "ingress": ing, "error": str(ex)[:300]})
     out = {
         "metric": "decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency",
         "value": res["value"],

@@ -147,7 +147,13 @@ __global__ __launch_bounds__(PROBE_BLOCK) void k_probe(
     // kernel of the batch touches them
     if (blockIdx.x == 0)
         for (uint32_t k = threadIdx.x; k < nhead; k += PROBE_BLOCK) head[k] = 0u;
-    if (RT) m = min(m, *ri.count);
+    if (RT) {
+        // a count above the caller's bound m_max: the requests past it get no
+        // result record -- reported, never silent (rl_engine_sync: RL_EOVERFLOW)
+        const uint32_t cnt = *ri.count;
+        if (cnt > m && blockIdx.x == 0 && threadIdx.x == 0) atomicOr(eflags, EF_ROUTED_OVER);
+        m = min(m, cnt);
+    }
     // a routed batch in received order (RL_ORDER_IDENTITY): request i is
     // rec[i], its store clock from its ts and the clock of the earlier steps
     const bool ident = RT && m && ri.order[0] == RL_ORDER_IDENTITY;
@@ -1317,6 +1323,7 @@ static int check_flags(rl_engine* e, uint32_t f) {
     if (f & EF_LOOKBACK) return fail(e, RL_ETIMEOUT, "radix sort look-back timed out");
     if (f & EF_ORDER) return fail(e, RL_EORDER, "per-key window ids went backwards");
     if (f & EF_INTERNAL) return fail(e, RL_EDEVICE, "cooperative replay invariant violated");
+    if (f & EF_ROUTED_OVER) return fail(e, RL_EOVERFLOW, "routed batch count above m_max: requests past it undecided");
     return RL_OK;
 }
 

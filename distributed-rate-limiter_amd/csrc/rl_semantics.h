@@ -32,6 +32,7 @@ enum : uint32_t {
     EF_LOOKBACK = 4u,         // radix-sort look-back spin bound hit
     EF_BAD_KEY = 8u,          // key id equal to the reserved empty marker
     EF_INTERNAL = 16u,        // cooperative replay invariant violated (never expected)
+    EF_ROUTED_OVER = 32u,     // a routed batch's device count exceeded m_max (requests past it undecided)
 };
 
 // Per-config constants, precomputed on the host exactly as Go computes them.

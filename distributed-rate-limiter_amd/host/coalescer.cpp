@@ -28,7 +28,7 @@ void Sub::carve(size_t m_) {
     status = RL_OK;
     op = OP_REQ;
     deadline = 0;
-    done = waiting = cancelled = dropped = in_queue = waited = false;
+    done = waiting = cancelled = dropped = truncated = in_queue = waited = false;
     inflight = 0;
     done_ns = submit_ns = 0;
     tag = nullptr;
@@ -404,6 +404,11 @@ void Coalescer::truncate_locked(Sub* s, int code) {
     // reaches the head of the queue
     const size_t rest = s->m - s->taken;
     if (rest == 0) return;
+    // the outcome is the context's error, whoever completes it: the results
+    // of the launched part are discarded and the tail never ran (its result
+    // arrays hold whatever a pooled Sub held before)
+    s->truncated = true;
+    s->status = code;
     pending_ -= rest;
     if (s->op == OP_REQ) (code == RL_ECANCELED ? st_.cancelled : st_.expired) += rest;
     s->taken = s->m;
@@ -446,7 +451,7 @@ int Coalescer::Wait(uint64_t ticket, int64_t timeout_ns, uint8_t* dec, int64_t* 
     for (;;) {
         if (s->cancelled) { code = RL_ECANCELED; break; }
         if (s->done) {
-            if (s->dropped) code = s->status;
+            if (s->dropped || s->truncated) code = s->status;
             break;
         }
         const int64_t now = steady_ns();
@@ -807,7 +812,7 @@ void Coalescer::completer() {
             st_.decided += s.is_reset ? 1 : s.m;
             for (const auto& p : s.parts) {
                 Sub* sub = p.sub;
-                if (st != RL_OK) sub->status = st;
+                if (st != RL_OK && !sub->truncated) sub->status = st;
                 sub->left -= p.count;
                 sub->inflight--;
                 if (sub->left == 0 && !sub->done) {

@@ -79,6 +79,7 @@ struct Sub {
     bool waiting = false;         // a caller blocks on cv (else completion skips the wake)
     bool cancelled = false;       // rl_coalescer_cancel before completion
     bool dropped = false;         // completed unapplied (deadline / cancel before launch)
+    bool truncated = false;       // launched in part; the rest dropped (deadline / cancel): no results
     bool in_queue = false;        // queue_ still holds it (the submitter pops it)
     bool waited = false;          // the caller released its ticket
     uint32_t inflight = 0;        // slot parts launched, not completed

@@ -715,8 +715,9 @@ class Coalescer:
             raise EngineError(rc, "rl_coalescer_submit failed")
         return t.value
 
-    def wait(self, ticket: int, m: int, timeout_ns=-1):
-        out = (np.empty(m, np.uint8), np.empty(m, np.int64), np.empty(m, np.int64), np.empty(m, np.int64))
+    def wait(self, ticket: int, m: int, timeout_ns=-1, out=None):
+        if out is None:
+            out = (np.empty(m, np.uint8), np.empty(m, np.int64), np.empty(m, np.int64), np.empty(m, np.int64))
         rc = lib.rl_coalescer_wait(self.h, ticket, timeout_ns, *[_ptr(x) for x in out])
         return rc, out
 

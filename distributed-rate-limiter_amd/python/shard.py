@@ -86,6 +86,20 @@ class RoutedPipeline:
     grouping of step b waited for step b - depth's unpack on the same step
     stream.)
 
+    Collective order (the first N > 1 run must not deadlock).  The request
+    collectives run on the request group (`pg_req`), the result collective on
+    `pg_res`: two communicators, two internal streams.  RCCL, like NCCL,
+    guarantees progress only when every rank runs the collectives of its
+    communicators in one consistent order (or every pending collective kernel
+    can be resident at once).  So the GPU order is made the host's issue
+    order, the same on every rank: each collective first waits for the last
+    one issued on the other group.  The result side of step b is issued
+    `lookahead` steps late, after step b + lookahead's request side, so the
+    one order is Req(0..L), Res(0), Req(L+1), Res(1), ...: a step's request
+    exchange never waits for the engine of the step before it, and its merge
+    and grouping wait only for the engine of step b - L - 1, which the
+    engine's three buffer sets make it wait for anyway at L = 1.
+
     decide(m_max, count, recv, order, sms, res, in_stream, out_stream) runs
     the owner's engine on the merged batch (rl_decide_routed_device_io;
     device pointers): the grouping waits for in_stream, out_stream waits for
@@ -95,7 +109,7 @@ class RoutedPipeline:
     the buckets and results are read in place)."""
 
     def __init__(self, ops, decide, world, max_batch, device, pg_req=None, pg_res=None, depth=4, exchange=None,
-                 staged=False):
+                 staged=False, lookahead=1):
         self.ops, self.decide, self.world = ops, decide, world
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
@@ -139,6 +153,15 @@ class RoutedPipeline:
                 ev_done=None,
             )
             self.slots.append(s)
+        # result sides issued `lookahead` steps late (exchange only: without
+        # collectives there is nothing to order)
+        self.lookahead = max(0, int(lookahead)) if self.exchange else 0
+        if depth <= self.lookahead:
+            raise ValueError("depth must exceed lookahead (a buffer set is reused after its step unpacked)")
+        self._pend = []               # (b, slot, m, dec, rem, retry, reset): result side not issued yet
+        self._ev_req = None           # after the last request-side collective issued (stream R)
+        self._ev_res = None           # after the last result-side collective issued (stream U)
+        self.order_log = []           # ("req" | "res", step): the collective issue order (tests)
         self.collectives = 0          # all-to-alls issued (tests: the exchange really ran)
         self.wait_s = 0.0             # host time spent waiting on the device: none by construction
         self.host_prof = {}
@@ -161,15 +184,25 @@ class RoutedPipeline:
         else:
             dist.all_to_all_single(out, inp, group=group)
 
+    def _record(self, stream):
+        if stream is None:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
+
     def step(self, b, key, ts, n, cfg, dec, rem, retry, reset):
-        """route, decide and return batch b (device tensors: key/ts/n int64,
-        cfg int32, complete now) into dec/rem/retry/reset (the caller's order);
-        returns the stream on which the results are complete"""
+        """route and decide batch b (device tensors: key/ts/n int64, cfg int32,
+        complete now); its results reach dec/rem/retry/reset (the caller's
+        order) once its result side is issued -- at once without the
+        exchange, else `lookahead` steps later or at flush().  Returns the
+        [(b', stream)] whose result sides this call issued: b' is complete on
+        `stream`."""
         s = self.slots[b % self.depth]
         m = key.numel()
         assert m <= self.max_batch
         p, sp = self._p, self._sp
-        R, U = self.R, self.U
+        R = self.R
         recv = s["recv"] if self.exchange else s["send"]
         rcnt = s["rcnt"] if self.exchange else s["scnt"]
         with _ctx(R):
@@ -177,25 +210,52 @@ class RoutedPipeline:
                 R.wait_event(s["ev_done"])   # the set's previous step has unpacked
             self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]), sp(R))
             if self.exchange:
+                if self._ev_res is not None:
+                    R.wait_event(self._ev_res)   # after the last result collective issued
                 self._a2a(s["rcnt"], s["scnt"], self.pg_req)
                 self._a2a(s["recv"], s["send"], self.pg_req)
+                self.order_log.append(("req", b))
+                self._ev_req = self._record(R)
             self.ops.merge(p(recv), p(rcnt), p(s["order"]), p(s["sms"]), p(s["count"]), sp(R))
             # the engine's grouping waits for R; U waits for its results
-            self.decide(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(R), sp(U))
+            self.decide(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(R),
+                        sp(self.U))
+        self._pend.append((b, s, m, dec, rem, retry, reset))
+        done = []
+        while len(self._pend) > self.lookahead:
+            done.append(self._result_side(*self._pend.pop(0)))
+        return done
+
+    def _result_side(self, b, s, m, dec, rem, retry, reset):
+        p, sp, U = self._p, self._sp, self.U
         with _ctx(U):
             if self.exchange:
+                if self._ev_req is not None:
+                    U.wait_event(self._ev_req)   # after the last request collective issued
                 self._a2a(s["back"], s["res"], self.pg_res)
+                self.order_log.append(("res", b))
+                self._ev_res = self._record(U)
             self.ops.unpack(m, p(s["slot"]), p(s["back"] if self.exchange else s["res"]), p(dec), p(rem), p(retry),
                             p(reset), sp(U))
             if U is not None:
                 s["ev_done"] = torch.cuda.Event()
                 s["ev_done"].record(U)
-        return U
+        return b, U
+
+    def flush(self):
+        """issue every deferred result side; returns [(b, stream)]"""
+        done = []
+        while self._pend:
+            done.append(self._result_side(*self._pend.pop(0)))
+        return done
 
     def run(self, batches, outs, done=None):
         """all batches through the pipeline: batches[b] = (key, ts, n, cfg),
         outs[b] = (dec, rem, retry, reset); `done(b, stream)` after each"""
         for b in range(len(batches)):
-            S = self.step(b, *batches[b], *outs[b])
+            for bd, S in self.step(b, *batches[b], *outs[b]):
+                if done is not None:
+                    done(bd, S)
+        for bd, S in self.flush():
             if done is not None:
-                done(b, S)
+                done(bd, S)

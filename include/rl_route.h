@@ -120,7 +120,12 @@ int rl_route_owner(rl_router* r, size_t m, const uint64_t* key, uint32_t* owner,
  * requests sent to o (<= cap), 1 the batch's earliest ts, 2 its latest ts
  * (INT64_MAX / INT64_MIN if the batch is empty), 3 twice the requests for o
  * dropped, plus 1 when the batch's ts decrease somewhere (a source in time
- * order needs no running max of its arrival times at the owner). */
+ * order needs no running max of its arrival times at the owner).  Rows 1-2
+ * cover the whole batch, dropped requests included: every owner must derive
+ * the same store clock, and a dropped request's time is still a time the
+ * shared store's clock (real time in the reference's single Redis) has
+ * reached -- so a dropped request advances the store clock like a sent one
+ * (tests/test_route_gpu.py::test_route_dropped_request_advances_store_clock). */
 int rl_route_pack(rl_router* r, size_t m, const uint64_t* key, const int64_t* ts, const int64_t* n,
                   const uint32_t* cfg, rl_route_rec* send, int64_t* send_info, uint32_t* slot, void* stream);
 
@@ -140,7 +145,10 @@ int rl_route_merge(rl_router* r, const rl_route_rec* recv, const int64_t* recv_i
 /* owner: the engine on the merged requests -- request p is recv[order[p]]
  * with store clock server_ms[p], p < *count (device memory, at most m_max <=
  * the engine's max_batch); its result goes to res[order[p]].  The grouping
- * waits for `stream` (the merge); `stream` waits for the results. */
+ * waits for `stream` (the merge); `stream` waits for the results.  m_max must
+ * be at least world * rl_router_capacity (the most a merge can count): a
+ * device count above m_max decides only the first m_max requests, and the
+ * next rl_engine_sync returns RL_EOVERFLOW. */
 int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
                             const uint32_t* order, const int64_t* server_ms, rl_route_res* res, void* stream);
 /* the same with the two sides on two streams: the grouping waits for

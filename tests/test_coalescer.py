@@ -305,6 +305,44 @@ def test_split_submission_context_end_drops_the_rest(rl, oracle_mod, how):
     assert (st.cancelled if how == "cancel" else st.expired) == 12
 
 
+def test_split_submission_deadline_unwaited_returns_the_deadline(rl, oracle_mod):
+    """the submitter truncates a split submission whose deadline passed while
+    its rest was queued and nobody waited (the gRPC server collects only after
+    completion): wait() then returns RL_EDEADLINE and copies no results -- the
+    tail never ran, so its result slots hold nothing of this submission"""
+    import time
+    be = GatedOracle(oracle_mod, CONFIGS[:1])
+    co = rl.Coalescer(be.batch, max_batch=8, max_in_flight=1)
+    # a pooled submission buffer left holding another request's results
+    t_prev = co.submit(np.arange(20, dtype=np.uint64) + 100, np.full(20, T0, np.int64), np.ones(20, np.int64),
+                       np.zeros(20, np.uint32))
+    assert co.wait(t_prev, 20)[0] == 0
+    be.entered.clear()
+    be.gate.clear()
+    m = 20
+    t = co.submit(np.full(m, 5, np.uint64), T0 + 1 + np.arange(m, dtype=np.int64), np.ones(m, np.int64),
+                  np.zeros(m, np.uint32), deadline_ns=rl.now_ns() + 30_000_000)
+    assert be.entered.wait(10)                      # the first 8 are on the "GPU"
+    time.sleep(0.06)                                # the deadline passes; nobody waits
+    be.gate.set()
+    time.sleep(0.1)                                 # the submitter meets the rest after the deadline
+    sentinel = (np.full(m, 0xAB, np.uint8),) + tuple(np.full(m, -7, np.int64) for _ in range(3))
+    rc = None
+    for _ in range(200):                            # completion without a waiter
+        rc, _ = co.wait(t, m, timeout_ns=0, out=sentinel)
+        if rc != rl.RL_ETIMEOUT:
+            break
+        time.sleep(0.01)
+    assert rc == rl.RL_EDEADLINE
+    assert (sentinel[0] == 0xAB).all() and all((x == -7).all() for x in sentinel[1:])   # nothing copied
+    assert co.wait(t, m)[0] == rl.RL_EINVAL         # the ticket is released
+    rc, (d, rem, _, _) = co.decide(5, T0 + 100, 1, 0)
+    st = co.stats()
+    co.close()
+    assert rc == 0 and rem == 20 - 8 - 1            # the other 12 never happened
+    assert st.expired == 12
+
+
 def test_cancelled_context_before_the_call(rl, oracle_mod):
     """interface_test.go:267-275: Allow with an already-cancelled context
     returns an error; the store is untouched"""

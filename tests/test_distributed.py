@@ -85,6 +85,11 @@ def _pipeline_worker(rank, world, port, q, m=3000, cap=4096, exchange=None):
                  for ob, eb in zip(outs, exp) for o, e in zip(ob, eb))
         # 3 collectives per step (info rows, records, results), nothing sized on the host
         ok = ok and pipe.exchange and pipe.collectives == 3 * len(mine) and pipe.wait_s == 0.0
+        # one collective order on every rank, across both groups: step b's
+        # result exchange between step b + 1's and b + 2's request exchanges
+        nb = len(mine)
+        want = [("req", 0)] + [x for b in range(1, nb) for x in (("req", b), ("res", b - 1))] + [("res", nb - 1)]
+        ok = ok and pipe.order_log == want
         q.put((rank, ok, ops.overflow))
     finally:
         dist.destroy_process_group()

@@ -262,6 +262,79 @@ def test_route_unpack_dropped_and_kept(rl):
     r.close()
 
 
+def test_route_dropped_request_advances_store_clock(rl):
+    """a request dropped at the sender (bucket overflow) still advances the
+    store clock to its time (include/rl_route.h): the shared store's clock is
+    the real time any app server has reached, sent or not -- so the next
+    step's requests expire keys at max(their time, the dropped request's)"""
+    import torch
+    rng = np.random.default_rng(31)
+    m = 3000
+    r = rl.Router(0, 1, m, 2048)
+    C = r.capacity
+    assert C < m
+    s = torch.cuda.current_stream().cuda_stream
+    late = T0 + 50_000_000_000                                   # the last request, 50 s later: dropped
+    ts1 = np.sort(T0 + rng.integers(0, 1_000_000_000, m).astype(np.int64))
+    ts1[-1] = late
+    ts2 = np.sort(T0 + 2_000_000_000 + rng.integers(0, 1_000_000_000, 100).astype(np.int64))
+    for step, ts in enumerate([ts1, ts2]):
+        k = rng.integers(0, 1 << 62, ts.size).astype(np.uint64)
+        kt, tt, nt, ct = _dev_tensors(torch, k, ts, np.ones(ts.size, np.int64), np.zeros(ts.size, np.uint32))
+        send = torch.empty((C, 4), dtype=torch.int64, device="cuda")
+        info = torch.empty((1, 4), dtype=torch.int64, device="cuda")
+        slot = torch.empty(ts.size, dtype=torch.int32, device="cuda")
+        r.pack(ts.size, kt.data_ptr(), tt.data_ptr(), nt.data_ptr(), ct.data_ptr(), send.data_ptr(),
+               info.data_ptr(), slot.data_ptr(), s)
+        order = torch.empty(C, dtype=torch.int32, device="cuda")
+        sms = torch.empty(C, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        r.merge(send.data_ptr(), info.data_ptr(), order.data_ptr(), sms.data_ptr(), cnt.data_ptr(), s)
+        torch.cuda.synchronize()
+        if step == 0:
+            assert int(info.cpu()[0, 2]) == late and int(slot.cpu()[-1]) == -1
+            assert r.sync(s) == rl.RL_EOVERFLOW
+        else:
+            assert int(order.cpu()[0]) == -1                      # identity form: sms[0] = earlier steps' clock
+            assert int(sms.cpu()[0]) == late // 1_000_000
+            assert r.sync(s) == rl.RL_OK
+    r.close()
+
+
+def test_routed_count_above_m_max_is_reported(rl):
+    """rl_decide_routed_device with m_max below the merged count decides only
+    the first m_max requests and says so: rl_engine_sync -> RL_EOVERFLOW"""
+    import torch
+    rng = np.random.default_rng(32)
+    m = 4096
+    r = rl.Router(0, 1, m, m)
+    C = r.capacity
+    eng = rl.Engine(profile=0, tb_capacity=1 << 14, win_capacity=1 << 12, max_batch=C)
+    for a, L, W in CONFIGS:
+        eng.register(a, L, W)
+    s = torch.cuda.current_stream().cuda_stream
+    ts = np.sort(T0 + rng.integers(0, 1_000_000_000, m).astype(np.int64))
+    k = rng.integers(0, 1000, m).astype(np.uint64)
+    kt, tt, nt, ct = _dev_tensors(torch, k, ts, np.ones(m, np.int64), (k % len(CONFIGS)).astype(np.uint32))
+    send = torch.empty((C, 4), dtype=torch.int64, device="cuda")
+    info = torch.empty((1, 4), dtype=torch.int64, device="cuda")
+    slot = torch.empty(m, dtype=torch.int32, device="cuda")
+    r.pack(m, kt.data_ptr(), tt.data_ptr(), nt.data_ptr(), ct.data_ptr(), send.data_ptr(), info.data_ptr(),
+           slot.data_ptr(), s)
+    order = torch.empty(C, dtype=torch.int32, device="cuda")
+    sms = torch.empty(C, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    res = torch.zeros((C, 4), dtype=torch.int64, device="cuda")
+    r.merge(send.data_ptr(), info.data_ptr(), order.data_ptr(), sms.data_ptr(), cnt.data_ptr(), s)
+    eng.decide_routed(m // 2, cnt.data_ptr(), send.data_ptr(), order.data_ptr(), sms.data_ptr(), res.data_ptr(), s, s)
+    torch.cuda.synchronize()
+    assert int(cnt.cpu()[0]) == m
+    assert eng.sync() == rl.RL_EOVERFLOW
+    assert eng.sync() == rl.RL_OK                                  # reported once, then cleared
+    eng.close()
+    r.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
