@@ -516,8 +516,16 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     for a, L, W in gen.configs:
         eng.register(a, L, W)
     exchange = world > 1 or args.route_exchange
-    pipe = shard.RoutedPipeline(router, eng.decide_routed, world, m, dev, pg_req=None, pg_res=pg_res,
-                                depth=int(os.environ.get("RL_ROUTE_DEPTH", "4")), exchange=exchange)
+    # A/B knobs: RL_ROUTE_LOOKAHEAD (result exchange that many steps late),
+    # RL_ROUTE_ONE_PG=1 (both directions on the default group: one stream
+    # orders them), RL_ROUTE_UNORDERED=1 (no cross-group waits)
+    one_pg = bool(os.environ.get("RL_ROUTE_ONE_PG"))
+    pipe = shard.RoutedPipeline(router, eng.decide_routed, world, m, dev, pg_req=None,
+                                pg_res=None if one_pg else pg_res,
+                                depth=int(os.environ.get("RL_ROUTE_DEPTH", "4")), exchange=exchange,
+                                lookahead=int(os.environ.get("RL_ROUTE_LOOKAHEAD", "1")),
+                                ordered=not os.environ.get("RL_ROUTE_UNORDERED"),
+                                decide_ev=None if os.environ.get("RL_ROUTE_NO_EV") else eng.decide_routed_ev)
     outs = [(torch.empty(m, dtype=torch.uint8, device=dev),) +
             tuple(torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)) for _ in range(pipe.depth)]
     def check(when):
@@ -565,7 +573,8 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
                     + "; merge and engine sized on the device, no host read in the step (include/rl_route.h)"),
         "batch": m,
         "bucket_capacity": router.capacity,
-        "collective_order": f"one order over both groups, result exchange {pipe.lookahead} step(s) late"
+        "collective_order": (("one group, one stream" if one_pg else "one order over both groups" if pipe.ordered
+                              else "unordered (A/B)") + f", result exchange {pipe.lookahead} step(s) late")
         if exchange else "none (world 1, buckets read in place)",
         "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
         "roofline": roof,
@@ -690,7 +699,7 @@ def main():
                             else "integer key ids")},
         "roofline": res["roofline"],
     }
-    for k in ("unique_keys_per_batch", "batches_in_flight", "bucket_capacity", "host_ms_per_step"):
+    for k in ("unique_keys_per_batch", "batches_in_flight", "bucket_capacity", "host_ms_per_step", "collective_order"):
         if k in res:
             out["config"][k] = res[k]
     for k in ("replay_detail", "latency", "stages_ms_per_batch", "stamp_ring"):

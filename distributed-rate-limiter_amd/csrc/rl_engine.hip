@@ -1033,7 +1033,8 @@ static int run_small(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
 // device memory; its inputs come from `s` (the merge)
 // s_out (nullable): the stream that waits for the results, when not s
 static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool inputs_ready,
-                     const KeyBytes* kb = nullptr, const RouteIn* ri = nullptr, hipStream_t s_out = nullptr) {
+                     const KeyBytes* kb = nullptr, const RouteIn* ri = nullptr, hipStream_t s_out = nullptr,
+                     hipEvent_t done_ev = nullptr) {
     if (m == 0) return RL_OK;
     if (m <= e->small_max && !e->timing && !ri) return run_small(e, m, a, s, inputs_ready, kb);
     const uint32_t* mdev = ri ? ri->count : nullptr;
@@ -1261,7 +1262,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     HIPCHK(e, hipMemsetAsync(B.zero + CTRL_HEAD, 0, e->zero_bytes - 4 * CTRL_HEAD, t));
     B.dirty = false;
     HIPCHK(e, hipEventRecord(B.back_done, t));
-    HIPCHK(e, hipStreamWaitEvent(s_out ? s_out : s, B.back_done, 0));
+    if (done_ev) HIPCHK(e, hipEventRecord(done_ev, t));   // the caller waits on it when it wants to
+    else HIPCHK(e, hipStreamWaitEvent(s_out ? s_out : s, B.back_done, 0));
     B.used = true;
     HIPCHK(e, hipGetLastError());
     e->stats.batches++;
@@ -1370,6 +1372,22 @@ extern "C" int rl_decide_routed_device_io(rl_engine* e, size_t m_max, const uint
     ReqArgs a{nullptr, nullptr, nullptr, nullptr, server_ms, nullptr, nullptr, nullptr, nullptr, nullptr};
     const RouteIn ri{recv, order, count, res};
     return run_batch(e, (uint32_t)m_max, a, s, false, nullptr, &ri, so);
+}
+
+extern "C" int rl_decide_routed_device_ev(rl_engine* e, size_t m_max, const uint32_t* count,
+                                          const rl_route_rec* recv, const uint32_t* order, const int64_t* server_ms,
+                                          rl_route_res* res, void* in_stream, void* done_event) {
+    if (!e || !count || !done_event || (m_max && (!recv || !order || !server_ms || !res))) return RL_EINVAL;
+    if (m_max > e->max_batch) return fail(e, RL_EINVAL, "routed batch bound above max_batch");
+    (void)hipSetDevice(e->device);
+    hipStream_t s = in_stream ? (hipStream_t)in_stream : e->stream;
+    if (!m_max) {   // nothing to decide: the event marks the caller's stream
+        HIPCHK(e, hipEventRecord((hipEvent_t)done_event, s));
+        return RL_OK;
+    }
+    ReqArgs a{nullptr, nullptr, nullptr, nullptr, server_ms, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const RouteIn ri{recv, order, count, res};
+    return run_batch(e, (uint32_t)m_max, a, s, false, nullptr, &ri, nullptr, (hipEvent_t)done_event);
 }
 
 extern "C" int rl_decide_routed_device(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,

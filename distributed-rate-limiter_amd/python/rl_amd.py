@@ -202,6 +202,7 @@ _sig = {
     "rl_route_unpack": (C.c_int, [vp, C.c_size_t] + [vp] * 7),
     "rl_decide_routed_device": (C.c_int, [vp, C.c_size_t] + [vp] * 6),
     "rl_decide_routed_device_io": (C.c_int, [vp, C.c_size_t] + [vp] * 7),
+    "rl_decide_routed_device_ev": (C.c_int, [vp, C.c_size_t] + [vp] * 7),
 }
 for _name, (_res, _args) in _sig.items():
     _f = getattr(lib, _name)
@@ -303,6 +304,13 @@ class Engine:
         else:
             rc = lib.rl_decide_routed_device_io(self.h, m_max, count_p, recv_p, order_p, sms_p, res_p, stream,
                                                 out_stream)
+        if rc != RL_OK:
+            raise EngineError(rc, self.last_error())
+
+    def decide_routed_ev(self, m_max, count_p, recv_p, order_p, sms_p, res_p, stream, event_p):
+        """rl_decide_routed_device_ev: the grouping waits for `stream`; the
+        results' completion is recorded into the hipEvent_t at event_p"""
+        rc = lib.rl_decide_routed_device_ev(self.h, m_max, count_p, recv_p, order_p, sms_p, res_p, stream, event_p)
         if rc != RL_OK:
             raise EngineError(rc, self.last_error())
 

@@ -109,7 +109,7 @@ class RoutedPipeline:
     the buckets and results are read in place)."""
 
     def __init__(self, ops, decide, world, max_batch, device, pg_req=None, pg_res=None, depth=4, exchange=None,
-                 staged=False, lookahead=1):
+                 staged=False, lookahead=1, ordered=True, decide_ev=None):
         self.ops, self.decide, self.world = ops, decide, world
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
@@ -136,6 +136,13 @@ class RoutedPipeline:
 
         self.R = new_stream()
         self.U = new_stream()
+        # decide_ev(m_max, count, recv, order, sms, res, in_stream, event):
+        # the engine records its results' completion into `event` instead of
+        # making U wait at call time -- with the result side issued
+        # `lookahead` steps late, a wait made at call time would queue U
+        # behind this step's engine before the result exchanges issued in
+        # between, and serialize the engine's steps
+        self.decide_ev = decide_ev if self.cuda else None
         self.slots = []
         for _ in range(depth):
             s = dict(
@@ -151,13 +158,18 @@ class RoutedPipeline:
                 res=torch.empty((tot, 4), dtype=torch.int64, device=d),
                 back=torch.empty((tot, 4), dtype=torch.int64, device=d) if self.exchange else None,
                 ev_done=None,
+                ev_res=None,
             )
+            if self.decide_ev is not None:
+                s["ev_res"] = torch.cuda.Event()
+                s["ev_res"].record(self.R)    # materialize the event: the engine records it from now on
             self.slots.append(s)
         # result sides issued `lookahead` steps late (exchange only: without
         # collectives there is nothing to order)
         self.lookahead = max(0, int(lookahead)) if self.exchange else 0
         if depth <= self.lookahead:
             raise ValueError("depth must exceed lookahead (a buffer set is reused after its step unpacked)")
+        self.ordered = bool(ordered)  # False: no cross-group waits (A/B only: the order is then unconstrained)
         self._pend = []               # (b, slot, m, dec, rem, retry, reset): result side not issued yet
         self._ev_req = None           # after the last request-side collective issued (stream R)
         self._ev_res = None           # after the last result-side collective issued (stream U)
@@ -210,7 +222,7 @@ class RoutedPipeline:
                 R.wait_event(s["ev_done"])   # the set's previous step has unpacked
             self.ops.pack(m, p(key), p(ts), p(n), p(cfg), p(s["send"]), p(s["scnt"]), p(s["slot"]), sp(R))
             if self.exchange:
-                if self._ev_res is not None:
+                if self._ev_res is not None and self.ordered and self.pg_res is not self.pg_req:
                     R.wait_event(self._ev_res)   # after the last result collective issued
                 self._a2a(s["rcnt"], s["scnt"], self.pg_req)
                 self._a2a(s["recv"], s["send"], self.pg_req)
@@ -218,8 +230,12 @@ class RoutedPipeline:
                 self._ev_req = self._record(R)
             self.ops.merge(p(recv), p(rcnt), p(s["order"]), p(s["sms"]), p(s["count"]), sp(R))
             # the engine's grouping waits for R; U waits for its results
-            self.decide(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(R),
-                        sp(self.U))
+            if self.decide_ev is not None:
+                self.decide_ev(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(R),
+                               s["ev_res"].cuda_event)
+            else:
+                self.decide(self.m_max, p(s["count"]), p(recv), p(s["order"]), p(s["sms"]), p(s["res"]), sp(R),
+                            sp(self.U))
         self._pend.append((b, s, m, dec, rem, retry, reset))
         done = []
         while len(self._pend) > self.lookahead:
@@ -229,8 +245,10 @@ class RoutedPipeline:
     def _result_side(self, b, s, m, dec, rem, retry, reset):
         p, sp, U = self._p, self._sp, self.U
         with _ctx(U):
+            if self.decide_ev is not None:
+                U.wait_event(s["ev_res"])        # this step's results (recorded by the engine)
             if self.exchange:
-                if self._ev_req is not None:
+                if self._ev_req is not None and self.ordered and self.pg_res is not self.pg_req:
                     U.wait_event(self._ev_req)   # after the last request collective issued
                 self._a2a(s["back"], s["res"], self.pg_res)
                 self.order_log.append(("res", b))

@@ -158,6 +158,15 @@ int rl_decide_routed_device_io(rl_engine* e, size_t m_max, const uint32_t* count
                                const uint32_t* order, const int64_t* server_ms, rl_route_res* res, void* in_stream,
                                void* out_stream);
 
+/* the same with the results' completion recorded into done_event (a
+ * hipEvent_t the caller owns) instead of a stream wait made at call time: a
+ * pipeline that issues its result side later (after the next step's request
+ * exchange) waits on the event then, so its result stream does not queue
+ * behind this batch before the collectives issued in between */
+int rl_decide_routed_device_ev(rl_engine* e, size_t m_max, const uint32_t* count, const rl_route_rec* recv,
+                               const uint32_t* order, const int64_t* server_ms, rl_route_res* res, void* in_stream,
+                               void* done_event);
+
 /* sender: back[world * cap] (the result buckets, send layout) -> the caller's
  * order; a dropped request gets decision RL_DROPPED and zeros */
 int rl_route_unpack(rl_router* r, size_t m, const uint32_t* slot, const rl_route_res* back, uint8_t* decision,

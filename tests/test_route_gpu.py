@@ -373,7 +373,7 @@ def _routed_rank(rank, world, port, backend, batches_of, q, exchange=None, cap=N
             eng.register(a, L, W)
         pg_res = dist.new_group(backend=backend)
         pipe = shard.RoutedPipeline(router, eng.decide_routed, world, mb, "cuda:0", pg_req=None, pg_res=pg_res,
-                                    exchange=exchange, staged=backend == "gloo")
+                                    exchange=exchange, staged=backend == "gloo", decide_ev=eng.decide_routed_ev)
         ins = [tuple(_dev_tensors(torch, *bt)) for bt in mine]
         outs = [(torch.empty(b[0].size, dtype=torch.uint8, device="cuda"),) +
                 tuple(torch.empty(b[0].size, dtype=torch.int64, device="cuda") for _ in range(3)) for b in mine]
