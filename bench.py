@@ -449,6 +449,10 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "coop_rounds": int(st.last_coop_rounds), "coop_iters": int(st.last_coop_iters),
                           "round_ends_full_stop_partial_first": [int(x) for x in st.coop_ends],
                           "exact_tiles": int(dbgw[20]), "serial_steps": int(dbgw[21]),
+                          # multi-decade windows: resolved, full, near passes, chain cycles / 16,
+                          # windows summarized XDEC / DEC, exact tiles, their passes, near
+                          # entries, near groups stopped unconverged
+                          "xdec": [int(x) for x in dbgw[60:70]],
                           # speculative restart windows: adopted, rejected (the chain's exit
                           # ended 1 / 2-64 steps after the guess, other)
                           "spec_windows": [int(dbgw[22]), int(dbgw[23]), int(dbgw[9]), int(dbgw[10]),

@@ -255,7 +255,7 @@ __device__ inline int64_t wave_incl_scan_i64(int64_t v) {
 constexpr int MAX_LCFG = 32;
 constexpr double TAU_DEC = 0.03;   // > 0.0222: far lanes are exact by the bound
 
-enum : int { QM_NONE = 0, QM_DEC = 1, QM_BIN = 2 };
+enum : int { QM_NONE = 0, QM_DEC = 1, QM_BIN = 2, QM_XDEC = 3 };   // QM_XDEC: rl_tb_xdec.h
 
 struct TbEval {
     double tokens;

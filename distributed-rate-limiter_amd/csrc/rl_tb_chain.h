@@ -52,11 +52,16 @@ constexpr int64_t DEC_LO = 10000000000000LL, DEC_HI = 100000000000000LL;
 constexpr int64_t BIN_LO = 1LL << 52, BIN_HI = 1LL << 53;
 constexpr uint32_t NO_STOP = 0xffffffffu;
 
+// 6 producers x 6 requests per lane: 8 waves per block, 2 per SIMD, so a
+// wave may hold 256 VGPRs.  With the multi-decade windows' code the 9-wave
+// shape (7 x 5, 168 VGPRs) spilled VGPRs into scratch memory inside the
+// chain's loops: configs[1] 2.48 vs 2.81e9, Zipf 1.5 8.7 vs 9.3e8
+// (profiles/r5_xdec_ab.txt)
 #ifndef RL_CH_NP
-#define RL_CH_NP 7
+#define RL_CH_NP 6
 #endif
 #ifndef RL_CH_K
-#define RL_CH_K 5
+#define RL_CH_K 6
 #endif
 constexpr int CH_K = RL_CH_K;                          // requests per producer lane
 constexpr int CH_NP = RL_CH_NP;                        // producer waves
@@ -79,6 +84,10 @@ constexpr int CH_SERIAL = 64;                          // serial exact steps per
 #define RL_CH_UNCHECKED 2
 #endif
 constexpr int CH_UNCHECKED = RL_CH_UNCHECKED;          // near fixed-point passes before the first convergence test
+#ifndef RL_XDEC
+#define RL_XDEC 1
+#endif
+constexpr bool CH_XDEC = RL_XDEC != 0;                 // multi-decade windows (rl_tb_xdec.h), Redis-7 profile
 #ifndef RL_HEAVY_G
 #define RL_HEAVY_G 2
 #endif
@@ -133,20 +142,32 @@ struct ChSpec {
     uint32_t valid;
     uint32_t first, cnt;   // window [first, first + cnt), summarized in tile[buf]
     uint32_t buf;
-    int32_t E;             // decimal mode at 10^(13 - E)
+    int32_t E;             // decimal mode at 10^(13 - E) (without XDEC windows)
+    double v0;             // XDEC: the guessed state after the exit (tokens): the window's plan starts there
+};
+
+// The window the producers summarized into tile[buf] (its representation:
+// the chain converts its exact state into it before resolving the window)
+struct ChWin {
+    int32_t mode;          // QM_DEC / QM_BIN / QM_XDEC
+    int32_t E;             // decade / binade, or the XDEC floor F
 };
 
 struct ChainShared {
     double2 r_add[RING_G];       // TbPre::add
     double2 r_th[RING_G];        // TbPre::th
     ChTile tile[2][CH_NP];
-    double ne_pred[2][CH_NP][CH_NE];   // tile-relative nominal predecessor of each near step
+    // near steps: tile-relative nominal predecessor (XDEC: int64 bits), add,
+    // th (XDEC: the step's nominal increment r, int64 bits)
+    double ne_pred[2][CH_NP][CH_NE];
     double ne_add[2][CH_NP][CH_NE];
     double ne_th[2][CH_NP][CH_NE];
+    uint64_t ne_kind[2][CH_NP];        // XDEC: bit k = near entry k is a reset step (a decade up)
     uint16_t ne_rank[2][CH_NP][64];    // near steps of the tile before each producer lane
     int32_t ne_off[CH_NP * CH_NE];     // chain: resolved offset after each near step
     ChState st[2];
     ChSpec spec[2];                    // producers' speculative window of the round
+    ChWin win[2];                      // the representation of tile[buf]'s window
 };
 
 __device__ inline double ring_add(const ChainShared& sh, uint32_t p) {
@@ -340,7 +361,7 @@ __device__ inline int32_t fast_mode(int64_t D, int32_t E, int32_t profile) {
     return (D >= BIN_LO && D < BIN_HI && E > -1000 && E < 900) ? QM_BIN : QM_NONE;
 }
 __device__ inline void mode_scale(int32_t mode, int32_t E, double& P, double& R) {
-    if (mode == QM_DEC) {
+    if (mode == QM_DEC || mode == QM_XDEC) {   // XDEC: the window's floor scale 10^(13 - F)
         P = rlq::pow10_exact(13 - E);
         R = 0.0;                           // the decimal step divides: no reciprocal
     } else {
@@ -553,9 +574,9 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
 // guess: the chain adopts the window only if its exact replay agrees
 // (ch_segment).
 __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainShared& sh, const ChState& s, double P,
-                                                                  double R, uint32_t j1) {
+                                                                  double R, uint32_t j1, bool xd) {
     constexpr int K = CH_K;
-    ChSpec sp{0u, 0u, 0u, 0u, 0};
+    ChSpec sp{0u, 0u, 0u, 0u, 0, 0.0};
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nt = (s.ccnt + CH_TILE - 1) / CH_TILE;
     const bool tv = lane < nt;
@@ -609,6 +630,15 @@ __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainSh
     const bool allow = sum >= thv;
     double post = allow ? sum - thv : sum;
     if (first >= j1 || !(post == post)) return sp;
+    if (xd) {
+        // multi-decade windows take any state after the exiting step: the
+        // window starts right after it, its plan from the guessed state
+        sp.valid = 1u;
+        sp.first = first;
+        sp.cnt = (j1 - first) < CH_W ? (j1 - first) : CH_W;
+        sp.v0 = post;
+        return sp;
+    }
     if (allow || !(post > 0.0)) {
         // the serial steps go on after an allow (the next step too) and while
         // the balance is at or below zero (off the fast decades): they end
@@ -651,6 +681,10 @@ __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainSh
     return sp;
 }
 
+}  // namespace rl
+#include "rl_tb_xdec.h"
+namespace rl {
+
 // ---------------------------------------------------------------------------
 // chain
 // ---------------------------------------------------------------------------
@@ -674,9 +708,9 @@ struct ChOutcome {
 // Resolve the chain window of state s (its tiles are in tile[s.cbuf]).
 template <int MODE>
 __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShared& sh, const ChState& s, double P,
-                                                                     double R, const ReqArgs& a, const TbRuns& runs,
-                                                                     uint32_t* eflags, uint32_t& iters,
-                                                                     uint32_t* dbg) {
+                                                                     double R, const XScale& xs, const ReqArgs& a,
+                                                                     const TbRuns& runs, uint32_t* eflags,
+                                                                     uint32_t& iters, uint32_t* dbg) {
     const uint32_t lane = threadIdx.x & 63;
 #ifdef RL_STAMPS
     const uint64_t t_in = __builtin_amdgcn_s_memtime();
@@ -701,7 +735,9 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
     uint32_t NPF[CH_NP];                                              // wave-uniform copies
 #pragma unroll
     for (int u = 0; u < CH_NP; u++) NPF[u] = (uint32_t)__builtin_amdgcn_readlane((int)np0, u);
-    const double tbase = (double)(s.D + TS_t);                        // nominal start of tile t
+    const int64_t tbase_i = s.D + TS_t;                               // nominal start of tile t
+    const double tbase = (double)tbase_i;                              // (exact in the one-decade modes)
+    uint32_t moff = 0;                                                 // XDEC: max |resolved offset|
 #ifdef RL_STAMPS
     if (dbg && lane == 0 && s.hot) atomicAdd(&dbg[39], (uint32_t)((__builtin_amdgcn_s_memtime() - t_in) >> 4));
 #endif
@@ -714,7 +750,82 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
     // no guess changes before the first step that leaves the regime, the
     // guesses are the true offsets (induction over lanes).
     uint32_t nstop = NO_STOP;
-    {
+    if constexpr (MODE == QM_XDEC) {
+        // The same fixed point on the window's integer states: a guess is the
+        // offset (exact - nominal) before the step; an add step reports its
+        // flip (exact result - (guessed predecessor + r)), a reset step (a
+        // decade up: its result forgets small errors of its predecessor) the
+        // offset after it, and a segmented scan turns both into the offset
+        // after every step.  No allow / clamp test here (th is not kept):
+        // a tile where one is possible never commits (ymin below), and its
+        // exact replay finds it.
+        constexpr int ITMAX = 16;
+        int32_t cbo = 0;
+        const uint32_t it_x0 = iters;
+        for (uint32_t b = 0; b < ne; b += 64) {
+            const uint32_t g = b + lane;
+            const bool v = g < ne;
+            uint32_t t = 0, base = NPF[0];
+#pragma unroll
+            for (int u = 1; u < CH_NP; u++) {
+                const bool ge = g >= NPF[u];
+                t += ge ? 1u : 0u;
+                base = ge ? NPF[u] : base;
+            }
+            const uint32_t k = v ? g - base : 0u;
+            const int64_t pn = __shfl(tbase_i, (int)t, 64) + __double_as_longlong(sh.ne_pred[cb][t][k]);
+            const double ad = sh.ne_add[cb][t][k];
+            const int64_t r = __double_as_longlong(sh.ne_th[cb][t][k]);
+            const bool rs = v && ((sh.ne_kind[cb][t] >> k) & 1ull);
+            int32_t est = cbo, outv = cbo;
+            uint32_t stop_lane = 64;
+            for (int it = 0;; it++) {
+                const int64_t pred = pn + est;
+                int64_t Xn = pred, Xin;
+                double tk;
+                bool up;
+                const bool ok = xstep(pred, xs, ad, __builtin_inf(), Xn, tk, up, Xin);
+                // flips from the state the step started from (the guess
+                // rounded onto a state), as in the one-decade modes
+                const int64_t d64 = rs ? Xn - (pn + r) : Xn - (Xin + r);
+                const bool brk = v && (!ok || d64 > 0x3fffffffLL || d64 < -0x3fffffffLL);
+                const bool fl = rs && !brk;
+                const int64_t incl = seg_incl_scan_i64(fl, (v && !brk) ? d64 : 0, (int64_t)cbo);
+                outv = (int32_t)incl;
+                int32_t en = (int32_t)__shfl_up(outv, 1, 64);   // the guess: the offset after the lane before
+                if (lane == 0) en = cbo;
+                iters++;
+                if (it + 1 < CH_UNCHECKED) {
+                    est = en;
+                    continue;
+                }
+                const uint32_t fb = first_lane(__ballot(brk));
+                const uint32_t fc = first_lane(__ballot(v && en != est));
+                if (fc >= fb) { stop_lane = fb; break; }
+                if (it + 1 == ITMAX) {
+                    stop_lane = fc;
+                    if (dbg && lane == 0) atomicAdd(&dbg[69], 1u);   // XDEC groups stopped unconverged
+                    break;
+                }
+                est = en;
+            }
+            const bool keep = v && lane < stop_lane;
+            if (keep) sh.ne_off[g] = outv;
+            const uint32_t ao = keep ? (uint32_t)(outv < 0 ? -outv : outv) : 0u;
+            moff = max(moff, (uint32_t)__builtin_amdgcn_readlane(
+                                 (int)wave_scan_u32(ao, 0u, [](uint32_t x, uint32_t y) { return x > y ? x : y; }), 63));
+            if (stop_lane < 64) {
+                nstop = b + stop_lane;
+                break;
+            }
+            cbo = __builtin_amdgcn_readlane(outv, 63);
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // ne_off visible to this wave
+        if (dbg && lane == 0) {   // dbg[62]: XDEC near passes, [68] near entries
+            atomicAdd(&dbg[62], iters - it_x0);
+            atomicAdd(&dbg[68], ne);
+        }
+    } else {
         constexpr int ITMAX = 16;
         int32_t cbo = 0;
         for (uint32_t b = 0; b < ne; b += 64) {
@@ -789,8 +900,17 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
     const int64_t D1 = Dt + T.S + (off_out - off_in);
     {
         const double dD = (double)Dt, nc = (double)T.nc;
-        const bool cand = forced || !(dD + nc + T.cmax < HI) || !(dD - nc + T.cmin >= LO + 1.0) ||
-                          !(dD + nc + 3.0 < T.ymin) || !(dD + nc + fmax(T.cmax, 0.0) <= T.dmax);
+        bool cand;
+        if constexpr (MODE == QM_XDEC) {
+            // the exact state stays within the producers' classification slack
+            // of their estimate V, and below every allow / clamp threshold:
+            // |X - V| <= |X_t - V_t| + drift + the tile's offset changes
+            const double bound = fabs(dD - T.cmax) + T.cmin + 2.0 * (double)moff + 4096.0;
+            cand = forced || !(bound < T.dmax) || !(bound + 2.0 < T.ymin);
+        } else {
+            cand = forced || !(dD + nc + T.cmax < HI) || !(dD - nc + T.cmin >= LO + 1.0) ||
+                   !(dD + nc + 3.0 < T.ymin) || !(dD + nc + fmax(T.cmax, 0.0) <= T.dmax);
+        }
         const uint64_t candm = __ballot(tv && cand);
         uint32_t lo = 0;                                   // tiles [lo, c) commit now
         uint32_t c = first_lane(candm);
@@ -799,7 +919,7 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
         for (;;) {
             if (tv && lane >= lo && lane < c) {
                 runs.len[pos] = (uint16_t)len;
-                runs.E[pos] = (int16_t)s.E;
+                runs.E[pos] = (int16_t)(MODE == QM_XDEC ? s.E + XRUN : s.E);
                 runs.D0[pos] = Dt;
                 runs.D1[pos] = D1;
             }
@@ -818,17 +938,24 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
             const uint32_t cn0 = (uint32_t)__builtin_amdgcn_readlane((int)np0, (int)c);
             const int32_t cin = (int32_t)__builtin_amdgcn_readlane(off_in, (int)c);
             int32_t goff = 0;
-            if (c < ovt) {
+            if (MODE != QM_XDEC && c < ovt) {
                 const uint32_t gi = cn0 + sh.ne_rank[cb][c][lane];
                 const uint32_t gc = gi < nres ? gi : nres;
                 goff = (gi > cn0 && gc) ? sh.ne_off[gc - 1] - cin : 0;
             }
+            (void)cin;
             int64_t Dq = 0;
 #ifdef RL_STAMPS
             const uint64_t t_ex = __builtin_amdgcn_s_memtime();
             const uint32_t it_ex = iters;
 #endif
-            uint32_t brk = exact_span<MODE, false>(RingSrc{sh}, cpos, clen, Dc, goff, P, R, Dq, a, iters);
+            uint32_t brk;
+            if constexpr (MODE == QM_XDEC) {
+                const uint32_t it_e = iters;
+                brk = exact_span_x<false>(RingSrc{sh}, cpos, clen, Dc, xs, Dq, a, iters);
+                if (dbg && lane == 0) atomicAdd(&dbg[67], iters - it_e);   // XDEC exact-tile passes
+            }
+            else brk = exact_span<MODE, false>(RingSrc{sh}, cpos, clen, Dc, goff, P, R, Dq, a, iters);
 #ifdef RL_STAMPS
             if (dbg && lane == 0 && s.hot) {   // [7] cycles / 16, [11] passes of the hot chain's exact tiles
                 atomicAdd(&dbg[7], (uint32_t)((__builtin_amdgcn_s_memtime() - t_ex) >> 4));
@@ -840,10 +967,10 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 brk = 0;
                 Dq = Dc;
             }
-            if (dbg && lane == 0) atomicAdd(&dbg[20], 1u);
+            if (dbg && lane == 0) atomicAdd(&dbg[MODE == QM_XDEC ? 66 : 20], 1u);
             if (lane == 0 && brk) {
                 runs.len[cpos] = (uint16_t)brk;
-                runs.E[cpos] = (int16_t)s.E;
+                runs.E[cpos] = (int16_t)(MODE == QM_XDEC ? s.E + XRUN : s.E);
                 runs.D0[cpos] = Dc;
                 runs.D1[cpos] = Dq;
             }
@@ -942,11 +1069,16 @@ struct SerialOut {
     uint32_t steps;
 };
 
+// xd: multi-decade windows are available -- stop after the forced steps
+// whenever the state fits one (any state of 1e-9 .. 1e12 tokens, or zero)
+__device__ inline bool xdec_fit(int64_t D, int32_t E) { return D == 0 || (E >= XDEC_FMIN && E <= XDEC_FMAX + 4); }
+
 template <typename AddAt, typename ThAt>
 __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt add_at, ThAt th_at, uint32_t q, int64_t D, int32_t E,
                                                                        bool force, uint32_t lim, uint32_t j1,
                                                                        const CfgDev* __restrict__ cfgs,
-                                                                       int32_t profile, const ReqArgs& a) {
+                                                                       int32_t profile, const ReqArgs& a,
+                                                                       bool xd = false) {
     const uint32_t lane = threadIdx.x & 63;
     // mode: the callers' fast regime (positive digits only).  emode: how a step
     // is evaluated here -- sign-symmetric, because %.14g / strtod and the
@@ -973,7 +1105,8 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
     uint32_t odec = 0;
     uint32_t g0 = q;       // first position of the outputs collected in the lanes
     uint32_t k = 0;
-    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || mode == QM_NONE); k++) {
+    for (; q < lim && k < (uint32_t)CH_SERIAL && (force || (mode == QM_NONE && !(xd && xdec_fit(xd ? (int64_t)Dd : D, E))));
+         k++) {
         const uint32_t kl = k & 63u;
         if (kl == 0) {
             if (k) {   // the previous 64 outputs
@@ -1012,7 +1145,7 @@ __device__ __attribute__((always_inline)) inline SerialOut serial_steps(AddAt ad
         }
         otok = lane == kl ? v.tokens : otok;
         odec = lane == kl ? (uint32_t)(v.allowed ? DEC_ALLOWED : DEC_DENIED) : odec;
-        force = v.allowed || v.clamped || !alive;
+        force = !xd && (v.allowed || v.clamped || !alive);
         const bool same = emode != QM_NONE && v.inrange;
         if (same) {
             D = v.Dact;                     // same decade / binade (sign may flip)
@@ -1272,6 +1405,38 @@ __device__ __attribute__((always_inline)) inline void wave_win_segment(WinEntry*
     }
 }
 
+// the chain's exact state (D, E, mode: its window's representation, or
+// stored digits for QM_DEC / QM_NONE) into the representation of window w;
+// false when it does not fit (then the state is left as it was)
+__device__ inline bool st_convert(ChState& s, const ChWin& w, int32_t profile) {
+    if (w.mode == QM_NONE) return false;
+    if (w.mode == s.mode && w.E == s.E) return true;
+    if (profile != PROFILE_REDIS7 || s.mode == QM_BIN || w.mode == QM_BIN) return false;
+    int64_t Dd = s.D;
+    int32_t Ed = s.E;
+    if (s.mode == QM_XDEC) x_to_dec(s.D, s.E, Dd, Ed);
+    int64_t out;
+    if (!dec_to_win(Dd, Ed, w.mode, w.E, out)) return false;
+    s.D = out;
+    s.E = w.E;
+    s.mode = w.mode;
+    return true;
+}
+// an estimate of the state (tokens) for a window's plan
+__device__ inline double st_value(int64_t D, int32_t E, int32_t mode) {
+    if (mode == QM_XDEC) return (double)D / rlq::pow10_exact(13 - E);
+    if (D == 0 || E < -9 || E > 13) return 0.0;
+    return (double)D / rlq::pow10_exact(13 - E);
+}
+
+// the multi-decade windows' resolution out of line: it is the rarer path,
+// and inlined its registers would crowd the one-decade path's
+__device__ __attribute__((always_inline)) inline ChOutcome ch_resolve_x(ChainShared& sh, const ChState& s, const XScale& xs,
+                                                          const ReqArgs& a, const TbRuns& runs, uint32_t* eflags,
+                                                          uint32_t& iters, uint32_t* dbg) {
+    return ch_resolve<QM_XDEC>(sh, s, xs.P[0], 0.0, xs, a, runs, eflags, iters, dbg);
+}
+
 // Replay one huge token-bucket segment [j0, j1) with the whole block.
 template <bool LCFG>
 __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh, TbEntry* e, uint32_t j0, uint32_t j1,
@@ -1311,14 +1476,25 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         }
     }
     lds_barrier();
+    const bool xd = CH_XDEC && profile == PROFILE_REDIS7;
     for (;;) {
         ChState s = sh.st[par];
+        // A window is resolved in the representation the producers summarized
+        // it in (sh.win): the chain's exact state at the window's start is
+        // converted into it.  nofit: it did not fit -- at least one exact
+        // serial step this round (progress whatever the plans say).
+        bool nofit = false;
         {
             const ChSpec sp = sh.spec[par];
             if (sp.valid) {
-                if (s.ccnt == 0 && s.mode == QM_DEC && s.pfirst == sp.first && s.E == sp.E) {
+                ChState t = s;
+                if (s.ccnt == 0 && s.pfirst == sp.first &&
+                    (xd ? st_convert(t, sh.win[sp.buf], profile) : (s.mode == QM_DEC && s.E == sp.E))) {
                     // the chain's exit ended where the producers guessed: their
                     // window is the next chain window
+                    s.D = t.D;
+                    s.E = t.E;
+                    s.mode = t.mode;
                     s.cfirst = sp.first;
                     s.ccnt = sp.cnt;
                     s.cbuf = sp.buf;
@@ -1340,46 +1516,88 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                         atomicAdd(&dbg[s.ccnt > 0 || s.pfirst <= sp.first || dd > 64u ? 15 : dd == 1u ? 9 : 10], 1u);
                     }
                 }
+            } else if (xd && s.ccnt > 0 && !st_convert(s, sh.win[s.cbuf], profile)) {
+                s.pfirst = s.cfirst;
+                s.ccnt = 0;
+                nofit = true;
             }
         }
         if (s.ccnt == 0 && s.pfirst >= j1) break;                 // block-uniform
-        const uint32_t pcnt = (s.mode != QM_NONE && s.pfirst < j1) ? ((j1 - s.pfirst) < CH_W ? (j1 - s.pfirst) : CH_W)
-                                                                   : 0u;
+        const bool fits = s.mode != QM_NONE || (xd && xdec_fit(s.D, s.E));
+        const uint32_t pcnt = (fits && !nofit && s.pfirst < j1) ? ((j1 - s.pfirst) < CH_W ? (j1 - s.pfirst) : CH_W)
+                                                                 : 0u;
         double P = 1.0, R = 1.0;
         if (s.mode != QM_NONE) mode_scale(s.mode, s.E, P, R);
         nrounds++;
         CH_T(t0);
         if (ch_producer_index(wave) >= 0) {
-            ChSpec sp{0u, 0u, 0u, 0u, 0};
-            if (s.ccnt > 0 && s.mode == QM_DEC) sp = ch_predict(sh, s, P, R, j1);
+            const uint32_t pw = (uint32_t)ch_producer_index(wave);
+            ChSpec sp{0u, 0u, 0u, 0u, 0, 0.0};
+            if (s.ccnt > 0 && s.mode == QM_DEC) sp = ch_predict(sh, s, P, R, j1, xd);
 #ifdef RL_STAMPS
             CH_T(t1);
             cyc[1] += t1 - t0;          // producers: the exit guess
             cyc[2] += sp.valid;         // producers: windows guessed
 #endif
-            if (ch_producer_index(wave) == 0 && (threadIdx.x & 63) == 0) {
-                sp.buf = s.pbuf;
-                sh.spec[par ^ 1u] = sp;
-            }
+            // the window to summarize and its representation
+            XPlan pl;
+            pl.mode = QM_NONE;
+            pl.E = 0;
+            uint32_t wf = 0, wc = 0;
+            double dmax = (double)DEC_HI;
             if (sp.valid) {
-                double P2, R2;
-                mode_scale(QM_DEC, sp.E, P2, R2);
-                ch_produce<QM_DEC>(sh, s.pbuf, ch_producer_index(wave), sp.first, sp.cnt, P2, (double)DEC_HI);
-            } else if (pcnt) {
-                if (s.mode == QM_DEC) {
-                    // bound on the window's states: the chain window's base plus
-                    // 2.25x its nominal growth (the chain verifies it per tile)
-                    double dmax = (double)DEC_HI;
-                    if (s.ccnt == CH_W) {
+                if (xd) {
+                    pl = ch_plan(sh, sp.first, sp.cnt, sp.v0);
+                    if (pl.mode == QM_NONE) sp.valid = 0u;
+                } else {
+                    pl.mode = QM_DEC;
+                    pl.E = sp.E;
+                }
+                wf = sp.first;
+                wc = sp.cnt;
+            }
+            if (!sp.valid && pcnt) {
+                wf = s.pfirst;
+                wc = pcnt;
+                if (s.mode == QM_DEC || s.mode == QM_BIN) {
+                    pl.mode = s.mode;
+                    pl.E = s.E;
+                    if (s.mode == QM_DEC && s.ccnt == CH_W) {
+                        // bound on the window's states: the chain window's base plus
+                        // 2.25x its nominal growth (the chain verifies it per tile)
                         int64_t G = 0;
 #pragma unroll
                         for (int t = 0; t < CH_NP; t++) G += sh.tile[s.cbuf][t].S;
                         dmax = fmin(dmax, (double)s.D + 2.25 * (double)(G > 0 ? G : 0) + 0x1p21);
                     }
-                    ch_produce<QM_DEC>(sh, s.pbuf, ch_producer_index(wave), s.pfirst, pcnt, P, dmax);
                 } else {
-                    ch_produce<QM_BIN>(sh, s.pbuf, ch_producer_index(wave), s.pfirst, pcnt, P, (double)BIN_HI);
+                    // after a multi-decade window or from a state off the fast
+                    // decades: plan from the state's estimate at the window start
+                    int64_t Xe = s.D;
+                    if (s.ccnt > 0) {
+                        const uint32_t nt = (s.ccnt + CH_TILE - 1) / CH_TILE;
+#pragma unroll
+                        for (int t = 0; t < CH_NP; t++) Xe += (uint32_t)t < nt ? sh.tile[s.cbuf][t].S : 0;
+                    }
+                    pl = ch_plan(sh, wf, wc, st_value(Xe, s.E, s.mode));
                 }
+            }
+            if (pw == 0 && (threadIdx.x & 63) == 0) {
+                sp.buf = s.pbuf;
+                sh.spec[par ^ 1u] = sp;
+                sh.win[s.pbuf] = ChWin{wc ? pl.mode : (int32_t)QM_NONE, pl.E};
+                // dbg[64 / 65]: windows summarized multi-decade / one-decade
+                if (dbg && wc) atomicAdd(&dbg[pl.mode == QM_XDEC ? 64 : 65], 1u);
+            }
+            if (wc && pl.mode == QM_XDEC) {
+                const XScale xs2 = xscale(pl.E);
+                ch_produce_x(sh, s.pbuf, pw, wf, wc, xs2, pick(pl.vt, pw));
+            } else if (wc && pl.mode == QM_DEC) {
+                double P2, R2;
+                mode_scale(QM_DEC, pl.E, P2, R2);
+                ch_produce<QM_DEC>(sh, s.pbuf, pw, wf, wc, P2, dmax);
+            } else if (wc && pl.mode == QM_BIN) {
+                ch_produce<QM_BIN>(sh, s.pbuf, pw, wf, wc, P, (double)BIN_HI);
             }
             __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             CH_T(t1);
@@ -1396,17 +1614,32 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             nx.pbuf = s.pbuf ^ 1u;
             nx.cbuf = s.pbuf;
             ChOutcome o{CH_PARTIAL, s.pfirst, s.D};
-            bool restart = true, force = false;
+            bool restart = true, force = nofit;
             if (s.ccnt > 0) {
-                o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, R, a, runs, eflags, iters, dbg)
-                                     : ch_resolve<QM_BIN>(sh, s, P, R, a, runs, eflags, iters, dbg);
+                if (s.mode == QM_XDEC) {
+                    const XScale xs = xscale(s.E);
+                    const uint64_t tx0 = __builtin_amdgcn_s_memtime();
+                    o = ch_resolve_x(sh, s, xs, a, runs, eflags, iters, dbg);
+                    // dbg[60..]: XDEC windows resolved, of them full, chain passes,
+                    // shader cycles / 16 (diagnostics)
+                    if (dbg && lane == 0) {
+                        atomicAdd(&dbg[60], 1u);
+                        atomicAdd(&dbg[61], o.kind == CH_FULL ? 1u : 0u);
+                        atomicAdd(&dbg[63], (uint32_t)((__builtin_amdgcn_s_memtime() - tx0) >> 4));
+                    }
+                } else {
+                    XScale xs;
+                    xs.F = 0;
+                    o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, R, xs, a, runs, eflags, iters, dbg)
+                                         : ch_resolve<QM_BIN>(sh, s, P, R, xs, a, runs, eflags, iters, dbg);
+                }
                 if (dbg && lane == 0) atomicAdd(&dbg[3 + o.kind], 1u);
                 CH_T(t1);
                 cyc[o.kind == CH_FULL ? 0 : 1] += t1 - t0;
                 t0 = t1;
                 if (o.kind == CH_FULL) {
                     restart = false;
-                    nx.D = o.D;                 // exact at s.pfirst
+                    nx.D = o.D;                 // exact at s.pfirst (the window's representation)
                 } else {
                     force = o.kind == CH_STOP;
                 }
@@ -1423,11 +1656,15 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 nx.pfirst = s.pfirst + pcnt;
             } else {
                 // exact serial steps: the exiting step, then on while the state
-                // is off the fast decades or the last step left the regime
+                // fits no window (off the fast decades, and with multi-decade
+                // windows also outside theirs) or the last step left the regime
                 const uint32_t lim = (j1 - s.pfirst) < CH_W ? j1 : s.pfirst + CH_W;   // resident in the ring
+                int64_t Dd = o.D;
+                int32_t Ed = s.E;
+                if (s.mode == QM_XDEC) x_to_dec(o.D, s.E, Dd, Ed);
                 const SerialOut so = serial_steps([&](uint32_t p) { return ring_add(sh, p); },
-                                                  [&](uint32_t p) { return ring_th(sh, p); }, o.q, o.D, s.E, force,
-                                                  lim, j1, cfgs, profile, a);
+                                                  [&](uint32_t p) { return ring_th(sh, p); }, o.q, Dd, Ed, force,
+                                                  lim, j1, cfgs, profile, a, xd);
                 nserial += so.steps;
                 CH_T(t1);
                 cyc[2] += t1 - t0;
@@ -1459,7 +1696,10 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
 #endif
     if (tid == 0) {
         const ChState s = sh.st[par];
-        tb_store_end(e, tb_value(s.D, s.E, profile), j1 - 1, cfgs, profile, a);
+        int64_t Dd = s.D;
+        int32_t Ed = s.E;
+        if (s.mode == QM_XDEC) x_to_dec(s.D, s.E, Dd, Ed);
+        tb_store_end(e, tb_value(Dd, Ed, profile), j1 - 1, cfgs, profile, a);
         if (dbg) {
             atomicAdd(&dbg[0], nrounds);
             atomicAdd(&dbg[1], iters);
@@ -1500,7 +1740,10 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
             int64_t Dend = 0;
             uint32_t brk;
             double P, R;
-            if (profile == PROFILE_REDIS7) {
+            if (profile == PROFILE_REDIS7 && E >= XRUN - 100) {     // a run of a multi-decade window
+                const XScale xs = xscale(E - XRUN);
+                brk = exact_span_x<true>(GlobSrc{pre.add, pre.th}, p, len, D0, xs, Dend, a, iters);
+            } else if (profile == PROFILE_REDIS7) {
                 mode_scale(QM_DEC, E, P, R);
                 brk = exact_span<QM_DEC, true>(GlobSrc{pre.add, pre.th}, p, len, D0, 0, P, R, Dend, a, iters);
             } else {
