@@ -501,7 +501,8 @@ constexpr uint32_t CTRL_HIST = CTRL_HEAD;             // [4][256]
 constexpr uint32_t CTRL_TILE = CTRL_HIST + 4 * RADIX;  // [4] tile counters
 constexpr uint32_t CTRL_UPB = CTRL_TILE + 4;          // [UP_NB] bucket fill counters (k_unpermute_bucket)
 constexpr uint32_t CTRL_PLAN = CTRL_UPB + UP_NB;      // [0] every MSD bucket fits k_sort_local [1] it does not
-constexpr uint32_t CTRL_WORDS = CTRL_PLAN + 2;
+constexpr uint32_t CTRL_XRUN = CTRL_PLAN + 2;         // runs of multi-decade chain windows listed (k_tb_expand_x)
+constexpr uint32_t CTRL_WORDS = CTRL_XRUN + 1;
 
 // The grouping sort's digits.  One pass: bits [0, 8).  More: the MSD pass
 // first, the top 8 bits [B - 8, B) of the B-bit slot ids, then either one
@@ -697,6 +698,7 @@ static void free_set(BatchSet& B) {
     (void)hipFree(B.o_tok);
     (void)hipFree(B.q_add); (void)hipFree(B.q_th);
     (void)hipFree(B.runs.len); (void)hipFree(B.runs.E); (void)hipFree(B.runs.D0); (void)hipFree(B.runs.D1);
+    (void)hipFree(B.runs.xlist);
     (void)hipFree(B.zero);
     (void)hipFree(B.kid);
     (void)hipFree(B.upb);
@@ -735,6 +737,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     ok &= hipMalloc(&B.runs.E, 2 * M) == hipSuccess;
     ok &= hipMalloc(&B.runs.D0, 8 * M) == hipSuccess;
     ok &= hipMalloc(&B.runs.D1, 8 * M) == hipSuccess;
+    ok &= hipMalloc(&B.runs.xlist, 4 * M) == hipSuccess;   // a run per start position at most
     ok &= hipMalloc(&B.zero, zero_bytes) == hipSuccess;
     ok &= hipMalloc(&B.upb, sizeof(UpRec) * std::min<size_t>(M, UP_MAX)) == hipSuccess;
     // front_done / chain_done only order the engine's own streams on this
@@ -747,6 +750,7 @@ static bool alloc_set(BatchSet& B, size_t M, size_t zero_bytes, size_t status_wo
     if (!ok) return false;
     B.ctrl = B.zero;
     B.status = B.zero + CTRL_WORDS;
+    B.runs.xcnt = B.ctrl + CTRL_XRUN;
     B.claim = B.status + status_words;
     // run lengths start at 0; k_tb_expand clears every one it consumes
     return hipMemset(B.runs.len, 0, 2 * M) == hipSuccess && hipMemset(B.zero, 0, zero_bytes) == hipSuccess;
@@ -1232,6 +1236,7 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     HIPCHK(e, hipStreamWaitEvent(t, chain_end, 0));
     if (tall) (void)hipEventRecord(ev[6], t);
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 4);
+    if (e->profile == PROFILE_REDIS7) k_tb_expand_x<<<32, 256, GROUP_LDS, t>>>(B.runs, ps, pre, e->d_eflags);
     k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
         m, B.runs, e->profile, ps, pre, e->d_eflags);
     if (ri) {

@@ -54,9 +54,9 @@ constexpr uint32_t NO_STOP = 0xffffffffu;
 
 // 6 producers x 6 requests per lane: 8 waves per block, 2 per SIMD, so a
 // wave may hold 256 VGPRs.  With the multi-decade windows' code the 9-wave
-// shape (7 x 5, 168 VGPRs) spilled VGPRs into scratch memory inside the
-// chain's loops: configs[1] 2.48 vs 2.81e9, Zipf 1.5 8.7 vs 9.3e8
-// (profiles/r5_xdec_ab.txt)
+// shape (7 x 5, at most 168 VGPRs) spilled inside the chain's loops even with
+// that code out of line: configs[1] 2.42 vs 2.80e9, Zipf 1.5 8.6 vs 9.4e8 on
+// one box (profiles/r5_xdec_ab.txt)
 #ifndef RL_CH_NP
 #define RL_CH_NP 6
 #endif
@@ -374,9 +374,11 @@ __device__ inline void mode_scale(int32_t mode, int32_t E, double& P, double& R)
 // (k_tb_expand's input; len is reset to 0 once the run is expanded)
 struct TbRuns {
     uint16_t* len;       // requests in the run starting here (0: none), <= CH_TILE
-    int16_t* E;          // decade / binade exponent
+    int16_t* E;          // decade / binade exponent (XDEC: the floor + XRUN)
     int64_t* D0;         // exact stored state before the run
     int64_t* D1;         // exact stored state after it, as the chain resolved it
+    uint32_t* xlist;     // start positions of the runs of multi-decade windows (k_tb_expand_x)
+    uint32_t* xcnt;      // their count (a zeroed control word of the batch set)
 };
 
 struct RingSrc {
@@ -703,6 +705,7 @@ struct ChOutcome {
     uint32_t kind;
     uint32_t q;        // FULL: window end; STOP: the exiting step; PARTIAL: end of the committed part
     int64_t D;         // exact stored digits before position q
+    uint32_t iters;    // ch_resolve_x: the caller's pass count after the call
 };
 
 // Resolve the chain window of state s (its tiles are in tile[s.cbuf]).
@@ -923,6 +926,15 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 runs.D0[pos] = Dt;
                 runs.D1[pos] = D1;
             }
+            if constexpr (MODE == QM_XDEC) {   // listed for k_tb_expand_x
+                const uint64_t cm = __ballot(tv && lane >= lo && lane < c);
+                if (cm) {
+                    uint32_t b0 = 0;
+                    if (lane == 0) b0 = atomicAdd(runs.xcnt, (uint32_t)__popcll(cm));
+                    b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+                    if ((cm >> lane) & 1ull) runs.xlist[b0 + (uint32_t)__popcll(cm & ((1ull << lane) - 1ull))] = pos;
+                }
+            }
             ChOutcome o;
             if (c >= nt) {
                 o.kind = CH_FULL;
@@ -973,6 +985,7 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 runs.E[cpos] = (int16_t)(MODE == QM_XDEC ? s.E + XRUN : s.E);
                 runs.D0[cpos] = Dc;
                 runs.D1[cpos] = Dq;
+                if (MODE == QM_XDEC) runs.xlist[atomicAdd(runs.xcnt, 1u)] = cpos;
             }
             if (brk < clen) {
                 o.kind = CH_STOP;
@@ -1203,6 +1216,46 @@ struct HeadSrc {
     __device__ double th(uint32_t p) const { return t[p]; }
 };
 
+// A multi-decade span of a heavy segment's wave, out of line (as the
+// chain's multi-decade work): from the exact stored state (D, E) off the fast
+// decades, up to CH_TILE requests at p with outputs, in a window whose floor
+// sits four decades below an upper bound of the span's states.  Returns the
+// requests replayed (the first one that leaves the regime, or len) and the
+// exact state before it in (D, E); 0 when no window fits.
+struct XSpan {
+    uint32_t brk;
+    int32_t E;
+    int64_t D;
+};
+__device__ XDEC_FN XSpan wave_span_x(HeadSrc src, uint32_t p, uint32_t len, int64_t D, int32_t E, ReqArgs a) {
+    constexpr int K = CH_K;
+    const uint32_t lane = threadIdx.x & 63;
+    XSpan o{0u, E, D};
+    double sa = 0.0;
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        const uint32_t i = lane * K + q;
+        const double ad = i < len ? src.add(p + i) : 0.0;
+        sa += fabs(ad) < 1e300 ? fabs(ad) : 0.0;
+    }
+    const double x0 = st_value(D, E, QM_NONE);
+    const double mx = fabs(x0) + wave_reduce_f64(sa, 0.0, [](double x, double y) { return x + y; });
+    if (!(mx < 1e12)) return o;
+    const int Et = mx > 0.0 ? (int)floor(log10(mx)) : XDEC_FMIN + 4;
+    const int F = max(Et - 4, XDEC_FMIN);
+    if (F > XDEC_FMAX) return o;
+    int64_t X0;
+    if (!dec_to_win(D, E, QM_XDEC, F, X0)) return o;
+    const XScale xs = xscale(F);
+    int64_t Xe = X0;
+    uint32_t iters = 0;
+    const uint32_t brk = exact_span_x<true>(src, p, len, X0, xs, Xe, a, iters);
+    if (brk > len) return o;   // (never) no convergence: the serial steps take over
+    x_to_dec(Xe, F, o.D, o.E);
+    o.brk = brk;
+    return o;
+}
+
 // Replay one heavy (not huge) token-bucket segment [j0, j1) with ONE wave:
 // exact_span over CH_TILE requests at a time, writing every result, and exact
 // serial steps wherever a step leaves the regime.  No producers, no runs:
@@ -1217,6 +1270,8 @@ __device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, u
     int32_t E = q0.E;
     int32_t mode = fast_mode(D, E, profile);
     uint32_t pos = j0;
+    const bool xd = CH_XDEC && profile == PROFILE_REDIS7;
+    bool exited = false;       // the last span stopped at a step that leaves the regime: a serial step next
     for (uint32_t guard = 0; pos < j1; guard++) {
         if (guard > 2u * (j1 - j0) + 8u) {        // each pass advances pos; never hang on it
             if ((threadIdx.x & 63) == 0) atomicOr(eflags, EF_INTERNAL | 0x100u);
@@ -1236,10 +1291,25 @@ __device__ __attribute__((always_inline)) inline void wave_segment(TbEntry* e, u
             D = readfirstlane_i64(Dq);
             pos += (uint32_t)__builtin_amdgcn_readfirstlane((int)brk);
             if (brk == len) continue;
+        } else if (xd && !exited && xdec_fit(D, E)) {
+            // off the fast decades (after an allow the balance random-walks
+            // across zero and decades): a multi-decade span, not serial steps
+            const uint32_t len = (j1 - pos) < CH_TILE ? (j1 - pos) : CH_TILE;
+            const XSpan xo = wave_span_x(src, pos, len, D, E, a);
+            const uint32_t brk = (uint32_t)__builtin_amdgcn_readfirstlane((int)xo.brk);
+            if (brk) {
+                D = readfirstlane_i64(xo.D);
+                E = __builtin_amdgcn_readfirstlane(xo.E);
+                mode = fast_mode(D, E, profile);
+                pos += brk;
+                exited = brk < len;
+                continue;
+            }
         }
+        exited = false;
         const SerialOut so = serial_steps([&](uint32_t p) { return src.add(p); }, [&](uint32_t p) { return src.th(p); },
                                           pos, D, E, true, j1, j1, cfgs,
-                                          profile, a);
+                                          profile, a, xd);
         // wave-uniform by construction; say so (the loop and its ballots stay uniform)
         pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)so.q);
         D = readfirstlane_i64(so.D);
@@ -1422,19 +1492,41 @@ __device__ inline bool st_convert(ChState& s, const ChWin& w, int32_t profile) {
     s.mode = w.mode;
     return true;
 }
-// an estimate of the state (tokens) for a window's plan
-__device__ inline double st_value(int64_t D, int32_t E, int32_t mode) {
-    if (mode == QM_XDEC) return (double)D / rlq::pow10_exact(13 - E);
-    if (D == 0 || E < -9 || E > 13) return 0.0;
-    return (double)D / rlq::pow10_exact(13 - E);
+
+// The multi-decade windows' work out of line (ch_resolve_x, ch_plan_w,
+// ch_produce_xw): it is the rarer path, and inlined into the chain kernel its
+// registers crowded the one-decade path's -- the 9-wave block (168 VGPRs)
+// spilled VGPRs into scratch inside the chain's loops, and an 8-wave block
+// cost the heavy / light phases 15 % on FW uniform (profiles/r5_xdec_ab.txt).
+// Called with the LDS state as an address-space-3 pointer, so their LDS
+// accesses stay ds_* instructions; everything else by value.
+typedef ChainShared __attribute__((address_space(3))) ChainLds;
+
+__device__ XDEC_FN ChOutcome ch_resolve_x(ChainLds* shp, ChState s, XScale xs, ReqArgs a,
+                                                          TbRuns runs, uint32_t* eflags, uint32_t iters,
+                                                          uint32_t* dbg) {
+    ChainShared& sh = *(ChainShared*)shp;
+    ChOutcome o = ch_resolve<QM_XDEC>(sh, s, xs.P[0], 0.0, xs, a, runs, eflags, iters, dbg);
+    o.iters = iters;
+    return o;
 }
 
-// the multi-decade windows' resolution out of line: it is the rarer path,
-// and inlined its registers would crowd the one-decade path's
-__device__ __attribute__((always_inline)) inline ChOutcome ch_resolve_x(ChainShared& sh, const ChState& s, const XScale& xs,
-                                                          const ReqArgs& a, const TbRuns& runs, uint32_t* eflags,
-                                                          uint32_t& iters, uint32_t* dbg) {
-    return ch_resolve<QM_XDEC>(sh, s, xs.P[0], 0.0, xs, a, runs, eflags, iters, dbg);
+struct XPlanW {
+    int32_t mode;
+    int32_t E;
+    double vt;        // the calling producer's tile start estimate
+};
+__device__ XDEC_FN XPlanW ch_plan_w(ChainLds* shp, uint32_t first, uint32_t cnt, double v0,
+                                                    uint32_t pw) {
+    const ChainShared& sh = *(const ChainShared*)shp;
+    const XPlan pl = ch_plan(sh, first, cnt, v0);
+    return XPlanW{pl.mode, pl.E, pick(pl.vt, pw)};
+}
+__device__ XDEC_FN void ch_produce_xw(ChainLds* shp, uint32_t buf, uint32_t t, uint32_t pfirst,
+                                                       uint32_t pcnt, int32_t F, double vt) {
+    ChainShared& sh = *(ChainShared*)shp;
+    const XScale xs = xscale(F);
+    ch_produce_x(sh, buf, t, pfirst, pcnt, xs, vt);
 }
 
 // Replay one huge token-bucket segment [j0, j1) with the whole block.
@@ -1540,14 +1632,16 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             cyc[2] += sp.valid;         // producers: windows guessed
 #endif
             // the window to summarize and its representation
-            XPlan pl;
+            ChainLds* const shl = (ChainLds*)&sh;
+            XPlanW pl;
             pl.mode = QM_NONE;
             pl.E = 0;
+            pl.vt = 0.0;
             uint32_t wf = 0, wc = 0;
             double dmax = (double)DEC_HI;
             if (sp.valid) {
                 if (xd) {
-                    pl = ch_plan(sh, sp.first, sp.cnt, sp.v0);
+                    pl = ch_plan_w(shl, sp.first, sp.cnt, sp.v0, pw);
                     if (pl.mode == QM_NONE) sp.valid = 0u;
                 } else {
                     pl.mode = QM_DEC;
@@ -1579,7 +1673,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
 #pragma unroll
                         for (int t = 0; t < CH_NP; t++) Xe += (uint32_t)t < nt ? sh.tile[s.cbuf][t].S : 0;
                     }
-                    pl = ch_plan(sh, wf, wc, st_value(Xe, s.E, s.mode));
+                    pl = ch_plan_w(shl, wf, wc, st_value(Xe, s.E, s.mode), pw);
                 }
             }
             if (pw == 0 && (threadIdx.x & 63) == 0) {
@@ -1590,8 +1684,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 if (dbg && wc) atomicAdd(&dbg[pl.mode == QM_XDEC ? 64 : 65], 1u);
             }
             if (wc && pl.mode == QM_XDEC) {
-                const XScale xs2 = xscale(pl.E);
-                ch_produce_x(sh, s.pbuf, pw, wf, wc, xs2, pick(pl.vt, pw));
+                ch_produce_xw(shl, s.pbuf, pw, wf, wc, pl.E, pl.vt);
             } else if (wc && pl.mode == QM_DEC) {
                 double P2, R2;
                 mode_scale(QM_DEC, pl.E, P2, R2);
@@ -1619,7 +1712,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 if (s.mode == QM_XDEC) {
                     const XScale xs = xscale(s.E);
                     const uint64_t tx0 = __builtin_amdgcn_s_memtime();
-                    o = ch_resolve_x(sh, s, xs, a, runs, eflags, iters, dbg);
+                    o = ch_resolve_x((ChainLds*)&sh, s, xs, a, runs, eflags, iters, dbg);
+                    iters = o.iters;
                     // dbg[60..]: XDEC windows resolved, of them full, chain passes,
                     // shader cycles / 16 (diagnostics)
                     if (dbg && lane == 0) {
@@ -1710,6 +1804,32 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     (void)eflags;
 }
 
+// Outputs of the multi-decade windows' runs (the chain lists them): one wave
+// per run, exact_span_x with outputs from the run's exact start, checked
+// against the end state the chain resolved.  A kernel of its own: inside
+// k_tb_expand its registers halved that kernel's occupancy, which every
+// batch's scan of the run starts pays for (mixed: 21 -> 38 us per batch,
+// profiles/r5_xdec_ab.txt).
+__global__ __launch_bounds__(256) void k_tb_expand_x(TbRuns runs, ReqArgs a, TbPre pre, uint32_t* eflags) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    const uint32_t n = *runs.xcnt;
+    uint32_t iters = 0;
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nw) {
+        const uint32_t p = runs.xlist[i];
+        const uint32_t len = runs.len[p];
+        const int32_t F = runs.E[p] - XRUN;
+        const int64_t D0 = runs.D0[p], D1 = runs.D1[p];
+        const XScale xs = xscale(F);
+        int64_t Dend = 0;
+        const uint32_t brk = exact_span_x<true>(GlobSrc{pre.add, pre.th}, p, len, D0, xs, Dend, a, iters);
+        if (lane == 0) {
+            if (brk != len || Dend != D1) atomicOr(eflags, EF_INTERNAL);
+            runs.len[p] = 0;
+        }
+    }
+}
+
 // Outputs of the committed runs: one wave per run, exact_span with outputs
 // from the run's exact start state, checked against the state the chain
 // resolved at the run's end.  Waves scan the batch in CH_TILE-position blocks and
@@ -1740,9 +1860,8 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
             int64_t Dend = 0;
             uint32_t brk;
             double P, R;
-            if (profile == PROFILE_REDIS7 && E >= XRUN - 100) {     // a run of a multi-decade window
-                const XScale xs = xscale(E - XRUN);
-                brk = exact_span_x<true>(GlobSrc{pre.add, pre.th}, p, len, D0, xs, Dend, a, iters);
+            if (profile == PROFILE_REDIS7 && E >= XRUN - 100) {     // a multi-decade window's: k_tb_expand_x
+                continue;
             } else if (profile == PROFILE_REDIS7) {
                 mode_scale(QM_DEC, E, P, R);
                 brk = exact_span<QM_DEC, true>(GlobSrc{pre.add, pre.th}, p, len, D0, 0, P, R, Dend, a, iters);
@@ -1782,7 +1901,9 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
     // blocks past grid_base join only a batch with a long light phase (many
     // distinct keys: every one a serial replay); otherwise they would only
     // take CUs from the next batch's grouping, which then bounds the step
-    if (blockIdx.x >= grid_base && nlight < light_min) return;
+    // (or many heavy segments: configs[0]'s 10k keys of ~100 requests, one
+    // per wave; light_min / 32 = m / 128 of them)
+    if (blockIdx.x >= grid_base && nlight < light_min && nheavy + nwin < light_min / 32u) return;
     // timeline (10 ns ticks, low 32 bits): dbg[13] = ~first block start,
     // dbg[14] = last block end, dbg[16/17] = longest segment start / end
     if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());

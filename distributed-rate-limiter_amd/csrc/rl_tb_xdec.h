@@ -43,6 +43,17 @@
 
 namespace rl {
 
+// the multi-decade work runs out of line in the chain kernel (see
+// ch_resolve_x in rl_tb_chain.h); RL_XDEC_OOL=0 inlines it (A/B only)
+#ifndef RL_XDEC_OOL
+#define RL_XDEC_OOL 1
+#endif
+#if RL_XDEC_OOL
+#define XDEC_FN __attribute__((noinline))
+#else
+#define XDEC_FN __attribute__((always_inline)) inline
+#endif
+
 constexpr int XDEC_FMIN = -9;          // 10^(13 - F) must be an exact double: 13 - F <= 22
 constexpr int XDEC_FMAX = 8;           // decades F .. F + 4 <= 12
 constexpr int16_t XRUN = 1000;         // TbRuns::E of a run committed in an XDEC window: F + XRUN
@@ -471,6 +482,13 @@ __device__ __attribute__((always_inline)) inline void ch_produce_x(ChainShared& 
         T.ev = ev_t;
         T.nc = ninc;
     }
+}
+
+// an estimate of the state (tokens) for a window's plan
+__device__ inline double st_value(int64_t D, int32_t E, int32_t mode) {
+    if (mode == QM_XDEC) return (double)D / rlq::pow10_exact(13 - E);
+    if (D == 0 || E < -9 || E > 13) return 0.0;
+    return (double)D / rlq::pow10_exact(13 - E);
 }
 
 // The exact state as stored digits (D, E): a window's representation -> a

@@ -235,12 +235,15 @@ def test_route_merge_one_source_in_order_is_identity(rl):
     r.close()
 
 
-def test_route_unpack_dropped_and_kept(rl):
+@pytest.mark.parametrize("m,shift", [(20_000, 0), (20_003, 0), (20_001, 1)])
+def test_route_unpack_dropped_and_kept(rl, m, shift):
+    """four requests per thread (ragged tails too), and unaligned outputs
+    (shift: every array one element in) through the one-per-thread kernel"""
     import torch
 
     import route_ops
-    rng = np.random.default_rng(5)
-    world, m, cap = 3, 20_000, 4096
+    rng = np.random.default_rng(5 + m)
+    world, cap = 3, 4096
     r = rl.Router(0, world, m, cap)
     C = r.capacity
     slot = rng.integers(0, world * C, m).astype(np.int32)
@@ -248,8 +251,9 @@ def test_route_unpack_dropped_and_kept(rl):
     back = rng.integers(-5, 1 << 40, (world * C, 4)).astype(np.int64)
     back[:, 0] = rng.integers(0, 4, world * C)
     st, bt = torch.from_numpy(slot).cuda(), torch.from_numpy(back).cuda()
-    outs = [torch.empty(m, dtype=torch.uint8, device="cuda")] + [torch.empty(m, dtype=torch.int64, device="cuda")
-                                                                 for _ in range(3)]
+    full = [torch.empty(m + shift, dtype=torch.uint8, device="cuda")] + \
+        [torch.empty(m + shift, dtype=torch.int64, device="cuda") for _ in range(3)]
+    outs = [x[shift:] for x in full]
     r.unpack(m, st.data_ptr(), bt.data_ptr(), *[x.data_ptr() for x in outs], torch.cuda.current_stream().cuda_stream)
     ops = route_ops.NumpyRouteOps(world, cap)
     outs_h = [torch.empty(m, dtype=torch.uint8)] + [torch.empty(m, dtype=torch.int64) for _ in range(3)]
