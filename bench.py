@@ -468,7 +468,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)
-                          "sort_predicted_batches": int(st.sort_predicted), "batches": int(st.batches)},
+                          "sort_predicted_batches": int(st.sort_predicted), "batches": int(st.batches),
+                          # replayed by the light kernel (no huge segment expected)
+                          "light_batches": int(st.light_batches)},
         "latency": latency,
         "stamp_ring": stamp_ring,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],

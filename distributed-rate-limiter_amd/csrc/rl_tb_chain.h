@@ -1877,18 +1877,89 @@ __global__ __launch_bounds__(256) void k_tb_expand(uint32_t m, TbRuns runs, int3
     }
 }
 
+// Phases 2 and 3 of the replay kernels: heavy token-bucket segments
+// (wave_segment) and heavy window segments (wave_win_segment), one per wave,
+// then light segments of any algorithm, one per thread, serial
+// (replay_*_serial).  nhx: huge token-bucket segments taken here as heavy
+// ones, ahead of them (k_replay_light; the chain kernel's phase 1 takes them
+// otherwise).  s_u: a __shared__ word of the calling kernel.
+__device__ __attribute__((always_inline)) inline void replay_rest(const uint32_t* __restrict__ sk, const SegLists& L,
+                                                                 uint32_t* qctr, uint32_t win_base, TbEntry* tb,
+                                                                 WinEntry* win, const Spill& spill,
+                                                                 const CfgDev* __restrict__ cfgs, int32_t profile,
+                                                                 const ReqArgs& a, const TbPre& pre, uint32_t* eflags,
+                                                                 uint32_t* dbg, uint32_t& s_u, uint32_t nhx) {
+    const uint32_t nheavy = L.count[0], nlight = L.count[1], nwin = L.count[2];
+    {
+        // heavy segments, HEAVY_G per claim: every wave's claim is an atomic on
+        // ONE counter, which sustains only ~88 atomics/us -- with one segment
+        // per claim, ten thousand short heavy segments (configs[0]'s keys)
+        // spent longer queueing on the counter than replaying
+        uint32_t iters = 0;
+        const uint32_t nhw = nhx + nheavy + nwin;
+        for (;;) {
+            uint32_t u0 = 0;
+            if ((threadIdx.x & 63) == 0) u0 = atomicAdd(&qctr[2], (uint32_t)HEAVY_G);
+            u0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0);
+            if (u0 >= nhw) break;
+            const uint32_t u1 = min(u0 + (uint32_t)HEAVY_G, nhw);
+            for (uint32_t u = u0; u < u1; u++) {
+                if (u < nhx + nheavy) {
+                    const SegRec sg = u < nhx ? L.list[3][u] : L.list[0][u - nhx];
+                    wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
+                } else {
+                    const SegRec sg = L.list[2][u - nhx - nheavy];
+                    wave_win_segment(&win[sk[sg.j0] - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a,
+                                     eflags);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)blockDim.x);
+        __syncthreads();
+        const uint32_t u0 = s_u;
+        __syncthreads();
+        if (u0 >= nlight) break;
+        const uint32_t u = u0 + threadIdx.x;
+        if (u < nlight) {
+            const SegRec sg = L.list[1][u];
+            const uint32_t k0 = sk[sg.j0];
+            // a key the batch inserted, alone in it: the absent state, unread
+            const bool fresh = sg.len == 1u && a.fresh && a.fresh[sg.j0];
+            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, fresh);
+            else replay_win_serial(&win[k0 - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags, fresh);
+        }
+    }
+    if (threadIdx.x == 0 && dbg) {
+        atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
+        atomicMax(&dbg[14], (uint32_t)__builtin_amdgcn_s_memrealtime());
+    }
+}
+
+// blocks past grid_base join only a batch with a long light phase (many
+// distinct keys: every one a serial replay), or with many heavy segments
+// (configs[0]'s 10k keys of ~100 requests, one per wave; light_min / 32 =
+// m / 128 of them); otherwise they would only take CUs from the next batch's
+// grouping, which then bounds the step
+__device__ inline bool replay_joins(const SegLists& L, uint32_t grid_base, uint32_t light_min) {
+    return blockIdx.x < grid_base || L.count[1] >= light_min || L.count[0] + L.count[2] >= light_min / 32u;
+}
+
 // The replay kernel.  Phase 1: huge token-bucket segments, one per block (the
-// chain), longest first.  Phase 2: heavy token-bucket segments (wave_segment)
-// and heavy window segments (wave_win_segment), one per wave.  Phase 3: light
-// segments of any algorithm, one per thread, serial (replay_*_serial).  The
-// hot keys' blocks stay in phase 1 while the others drain phases 2-3.
+// chain), longest first; then replay_rest.  The hot keys' blocks stay in
+// phase 1 while the others drain phases 2-3.  h_huge: a host-mapped word, the
+// batch's count of huge segments (the host launches k_replay_light when the
+// last replay it saw had none).
 template <bool LCFG>
 __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restrict__ sk, SegLists L, uint32_t* qctr,
                                                        uint32_t win_base, TbEntry* tb, WinEntry* win, Spill spill,
                                                        const CfgDev* __restrict__ gcfgs, uint32_t ncfg,
                                                        int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
                                                        uint32_t* dbg, TbRuns runs, uint32_t grid_base,
-                                                       uint32_t light_min) {
+                                                       uint32_t light_min, uint32_t* h_huge) {
     __shared__ ChainShared sh;
     __shared__ uint32_t s_u;
     __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
@@ -1897,13 +1968,9 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         __syncthreads();
     }
     const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
-    const uint32_t nheavy = L.count[0], nlight = L.count[1], nwin = L.count[2], nhuge = L.count[3];
-    // blocks past grid_base join only a batch with a long light phase (many
-    // distinct keys: every one a serial replay); otherwise they would only
-    // take CUs from the next batch's grouping, which then bounds the step
-    // (or many heavy segments: configs[0]'s 10k keys of ~100 requests, one
-    // per wave; light_min / 32 = m / 128 of them)
-    if (blockIdx.x >= grid_base && nlight < light_min && nheavy + nwin < light_min / 32u) return;
+    const uint32_t nhuge = L.count[3];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && h_huge) *(volatile uint32_t*)h_huge = nhuge;
+    if (!replay_joins(L, grid_base, light_min)) return;
     // timeline (10 ns ticks, low 32 bits): dbg[13] = ~first block start,
     // dbg[14] = last block end, dbg[16/17] = longest segment start / end
     if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
@@ -1959,53 +2026,40 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
             }
         }
     }
-    {
-        // heavy segments, HEAVY_G per claim: every wave's claim is an atomic on
-        // ONE counter, which sustains only ~88 atomics/us -- with one segment
-        // per claim, ten thousand short heavy segments (configs[0]'s keys)
-        // spent longer queueing on the counter than replaying
-        uint32_t iters = 0;
-        const uint32_t nhw = nheavy + nwin;
-        for (;;) {
-            uint32_t u0 = 0;
-            if ((threadIdx.x & 63) == 0) u0 = atomicAdd(&qctr[2], (uint32_t)HEAVY_G);
-            u0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)u0);
-            if (u0 >= nhw) break;
-            const uint32_t u1 = min(u0 + (uint32_t)HEAVY_G, nhw);
-            for (uint32_t u = u0; u < u1; u++) {
-                if (u < nheavy) {
-                    const SegRec sg = L.list[0][u];
-                    wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
-                } else {
-                    const SegRec sg = L.list[2][u - nheavy];
-                    wave_win_segment(&win[sk[sg.j0] - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a,
-                                     eflags);
-                }
-            }
-        }
-    }
-    __syncthreads();
-    const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)CH_BLOCK);
+    replay_rest(sk, L, qctr, win_base, tb, win, spill, cfgs, profile, a, pre, eflags, dbg, s_u, 0u);
+}
+
+// The replay kernel of a batch with no huge segment expected (the last
+// replay the host saw had none: mixed, uniform and bursty traffic): phases 2-3
+// only, in blocks of LT_BLOCK threads -- without the chain's 156 KB of LDS and
+// its register budget, a CU holds 12 replay waves instead of 8.  A huge
+// segment that arrives anyway is replayed as a heavy one (wave_segment:
+// exact, one wave), and the host word makes the next batches take the chain
+// kernel again.
+#ifndef RL_LT_BLOCK
+#define RL_LT_BLOCK 768
+#endif
+constexpr int LT_BLOCK = RL_LT_BLOCK;
+template <bool LCFG>
+__global__ __launch_bounds__(LT_BLOCK) void k_replay_light(const uint32_t* __restrict__ sk, SegLists L, uint32_t* qctr,
+                                                           uint32_t win_base, TbEntry* tb, WinEntry* win, Spill spill,
+                                                           const CfgDev* __restrict__ gcfgs, uint32_t ncfg,
+                                                           int32_t profile, ReqArgs a, TbPre pre, uint32_t* eflags,
+                                                           uint32_t* dbg, TbRuns runs, uint32_t grid_base,
+                                                           uint32_t light_min, uint32_t* h_huge) {
+    __shared__ uint32_t s_u;
+    __shared__ CfgDev s_cfg[LCFG ? MAX_LCFG : 1];
+    if (LCFG) {
+        for (uint32_t c = threadIdx.x; c < ncfg; c += blockDim.x) s_cfg[c] = gcfgs[c];
         __syncthreads();
-        const uint32_t u0 = s_u;
-        __syncthreads();
-        if (u0 >= nlight) break;
-        const uint32_t u = u0 + threadIdx.x;
-        if (u < nlight) {
-            const SegRec sg = L.list[1][u];
-            const uint32_t k0 = sk[sg.j0];
-            // a key the batch inserted, alone in it: the absent state, unread
-            const bool fresh = sg.len == 1u && a.fresh && a.fresh[sg.j0];
-            if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, fresh);
-            else replay_win_serial(&win[k0 - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags, fresh);
-        }
     }
-    if (threadIdx.x == 0 && dbg) {
-        atomicMax(&dbg[12], (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_light));
-        atomicMax(&dbg[14], (uint32_t)__builtin_amdgcn_s_memrealtime());
-    }
+    (void)runs;
+    const CfgDev* cfgs = LCFG ? s_cfg : gcfgs;
+    const uint32_t nhuge = L.count[3];
+    if (blockIdx.x == 0 && threadIdx.x == 0 && h_huge) *(volatile uint32_t*)h_huge = nhuge;
+    if (!replay_joins(L, grid_base, light_min)) return;
+    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
+    replay_rest(sk, L, qctr, win_base, tb, win, spill, cfgs, profile, a, pre, eflags, dbg, s_u, nhuge);
 }
 
 }  // namespace rl

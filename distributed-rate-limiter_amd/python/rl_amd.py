@@ -71,6 +71,7 @@ class rl_stats(_Sized):
         ("stamp_cycles", C.c_uint64 * 7),
         ("coop_ends", C.c_uint64 * 4),
         ("sort_predicted", C.c_uint64),
+        ("light_batches", C.c_uint64),
     ]
 
 

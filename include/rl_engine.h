@@ -101,6 +101,7 @@ typedef struct rl_stats {
                                   (exact-pass mismatch safety net), [3] offset iteration cap */
     uint64_t sort_predicted;   /* batches whose grouping sort was launched as k_sort_local only (every
                                   MSD bucket predicted to fit LDS: no LSD passes, no k_segments) */
+    uint64_t light_batches;    /* batches replayed by the light replay kernel (no huge segment expected) */
 } rl_stats;
 
 /* replaces redis.NewClient + NewTokenBucket/NewSlidingWindow/NewFixedWindow's
