@@ -1657,12 +1657,22 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                     pl.mode = s.mode;
                     pl.E = s.E;
                     if (s.mode == QM_DEC && s.ccnt == CH_W) {
-                        // bound on the window's states: the chain window's base plus
-                        // 2.25x its nominal growth (the chain verifies it per tile)
+                        // bound on the window's states (the chain verifies it per
+                        // tile): from the chain window's base, its nominal growth G
+                        // plus the larger of 1.25 G and 1.5 x its peak above its
+                        // start.  Round 4 took 2.25 G alone: one hot key's states
+                        // climb ~4e-3 tokens per window under a +-2e-3 sawtooth of
+                        // last_refill's rounding, which broke the bound in ~40 % of
+                        // its tiles -- each then replayed exactly
                         int64_t G = 0;
+                        double pk = 0.0;
 #pragma unroll
-                        for (int t = 0; t < CH_NP; t++) G += sh.tile[s.cbuf][t].S;
-                        dmax = fmin(dmax, (double)s.D + 2.25 * (double)(G > 0 ? G : 0) + 0x1p21);
+                        for (int t = 0; t < CH_NP; t++) {
+                            pk = fmax(pk, (double)G + sh.tile[s.cbuf][t].cmax);
+                            G += sh.tile[s.cbuf][t].S;
+                        }
+                        const double g = (double)(G > 0 ? G : 0);
+                        dmax = fmin(dmax, (double)s.D + g + fmax(1.25 * g, 1.5 * pk) + 0x1p21);
                     }
                 } else {
                     // after a multi-decade window or from a state off the fast
