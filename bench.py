@@ -466,6 +466,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                                                  "stamp_after": (((int(dbgw[19]) - (~int(dbgw[13]) & 0xffffffff) + (1 << 31)) & 0xffffffff) - (1 << 31)) / 100 if dbgw[19] else None},
                           "stamps_x16": [int(x) * 16 for x in dbgw[24:37]], "near_hot": [int(x) for x in dbgw[37:39]],
                           "near_setup_x16": int(dbgw[39]) * 16,
+                          # stamps build: producer 0's cycles on one-decade / multi-decade windows and their
+                          # counts, then the chain's resolve cycles and counts the same way
+                          "split_x16": [int(dbgw[70 + k]) * (16 if k in (0, 1, 4, 5) else 1) for k in range(8)],
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)

@@ -1272,9 +1272,13 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     HIPCHK(e, hipStreamWaitEvent(t, chain_end, 0));
     if (tall) (void)hipEventRecord(ev[6], t);
     if (sr) k_stamp<<<1, 64, 0, t>>>(sr + 4);
-    if (e->profile == PROFILE_REDIS7) k_tb_expand_x<<<32, 256, GROUP_LDS, t>>>(B.runs, ps, pre, e->d_eflags);
-    k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
-        m, B.runs, e->profile, ps, pre, e->d_eflags);
+    // runs come from the chain only: a light replay leaves none to expand
+    // (mixed: 24 + 7 us per batch off the finish stream)
+    if (!light) {
+        if (e->profile == PROFILE_REDIS7) k_tb_expand_x<<<32, 256, GROUP_LDS, t>>>(B.runs, ps, pre, e->d_eflags);
+        k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
+            m, B.runs, e->profile, ps, pre, e->d_eflags);
+    }
     if (ri) {
         // a routed batch: one result record per request at its receive
         // index, through merge-position buckets (no scattered 32-byte stores:

@@ -329,6 +329,22 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
     return d;
 }
 
+// x / P correctly rounded (as IEEE division) for an integer-valued |x| < 2^47,
+// P = 10^k (1 <= k <= 22, exact) and R = RN(1/P), in five dependent
+// operations instead of the division's eleven.  q1 = q0 + r R corrects the
+// product q0 = RN(x R) to within 1/2 ulp + 2^-51 ulp of x/P; the residual
+// r1 = x - q1 P is then exact (|r1| <= 0.51 ulp(q1) P < 2^53 units of
+// ulp(q1) ulp(P), as every 10^k has a mantissa below 2), and q1 + r1 R is
+// within 2^-54 ulp of x/P.  x/P = x / (2^k 5^k) with x an integer below
+// 2^47 is never a rounding midpoint and lies at least ulp / (2 5^k) >=
+// 2.1e-16 ulp from one (k <= 22), so the final rounding is RN(x/P).
+// Checked against IEEE division on 1.4e9 random (x, k): scripts/div_p10_check.c.
+__device__ __attribute__((always_inline)) inline double div_p10(double x, double P, double R) {
+    const double q0 = x * R;
+    const double q1 = __builtin_fma(__builtin_fma(-q0, P, x), R, q0);
+    return __builtin_fma(__builtin_fma(-q1, P, x), R, q1);
+}
+
 // The live-key step from stored digits Dpred (exact integer-valued double,
 // positive, in the decade/binade of P) in a fast mode: tokens (the
 // unquantized double) and the next stored digits D' -- NaN when the step
@@ -337,9 +353,9 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
 template <int MODE>
 __device__ inline double tb_step_d(double Dpred, double P, double R, double add, double th, double& tokens) {
     // strtod("D e(E-13)"): D < 2^47 and P = 10^k (k <= 22) are exact doubles,
-    // so one correctly rounded IEEE division is strtod's result (Clinger's
-    // fast path)
-    const double T = MODE == QM_DEC ? Dpred / P : Dpred * R;        // binary: exact, R = 2^E
+    // so one correctly rounded division is strtod's result (Clinger's fast
+    // path): div_p10 with R = RN(1/P) (mode_scale)
+    const double T = MODE == QM_DEC ? div_p10(Dpred, P, R) : Dpred * R;   // binary: exact, R = 2^E
     const double sum = T + add;
     tokens = sum;
     double Dn;
@@ -363,7 +379,7 @@ __device__ inline int32_t fast_mode(int64_t D, int32_t E, int32_t profile) {
 __device__ inline void mode_scale(int32_t mode, int32_t E, double& P, double& R) {
     if (mode == QM_DEC || mode == QM_XDEC) {   // XDEC: the window's floor scale 10^(13 - F)
         P = rlq::pow10_exact(13 - E);
-        R = 0.0;                           // the decimal step divides: no reciprocal
+        R = 1.0 / P;                       // RN(1/P): the decimal step's div_p10
     } else {
         P = ldexp(1.0, -E);
         R = ldexp(1.0, E);
@@ -1538,6 +1554,12 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t nrounds = 0, iters = 0, par = 0, nserial = 0;
     uint64_t cyc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0;
+#ifdef RL_STAMPS
+    // dbg[70..79] (producer 0 / chain wave, segments >= 65536): producer cycles
+    // of one-decade / multi-decade windows and their counts, chain resolve
+    // cycles of one-decade / multi-decade windows and their counts
+    uint64_t cx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     (void)t0; (void)t1;
     TbLoader L;
     L.next = j0 / 128u;
@@ -1618,8 +1640,12 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         const bool fits = s.mode != QM_NONE || (xd && xdec_fit(s.D, s.E));
         const uint32_t pcnt = (fits && !nofit && s.pfirst < j1) ? ((j1 - s.pfirst) < CH_W ? (j1 - s.pfirst) : CH_W)
                                                                  : 0u;
+        // the scale (the decimal modes' reciprocal only where the chain
+        // resolves a window: a division on every wave's round is ~1 % of the
+        // producers' round)
         double P = 1.0, R = 1.0;
-        if (s.mode != QM_NONE) mode_scale(s.mode, s.E, P, R);
+        if (s.mode == QM_BIN) mode_scale(s.mode, s.E, P, R);
+        else if (s.mode != QM_NONE) P = rlq::pow10_exact(13 - s.E);
         nrounds++;
         CH_T(t0);
         if (ch_producer_index(wave) >= 0) {
@@ -1693,17 +1719,26 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 // dbg[64 / 65]: windows summarized multi-decade / one-decade
                 if (dbg && wc) atomicAdd(&dbg[pl.mode == QM_XDEC ? 64 : 65], 1u);
             }
+#ifdef RL_STAMPS
+            uint64_t tp0;
+            CH_T(tp0);
+#endif
             if (wc && pl.mode == QM_XDEC) {
                 ch_produce_xw(shl, s.pbuf, pw, wf, wc, pl.E, pl.vt);
             } else if (wc && pl.mode == QM_DEC) {
-                double P2, R2;
-                mode_scale(QM_DEC, pl.E, P2, R2);
-                ch_produce<QM_DEC>(sh, s.pbuf, pw, wf, wc, P2, dmax);
+                ch_produce<QM_DEC>(sh, s.pbuf, pw, wf, wc, rlq::pow10_exact(13 - pl.E), dmax);
             } else if (wc && pl.mode == QM_BIN) {
                 ch_produce<QM_BIN>(sh, s.pbuf, pw, wf, wc, P, (double)BIN_HI);
             }
             __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             CH_T(t1);
+#ifdef RL_STAMPS
+            if (wc) {
+                const int xk = pl.mode == QM_XDEC ? 1 : 0;
+                cx[xk] += t1 - tp0;
+                cx[2 + xk] += 1;
+            }
+#endif
             cyc[0] += t1 - t0;
         } else if (wave == (uint32_t)CH_LOADER) {
             const uint32_t first = s.ccnt ? s.cfirst : s.pfirst;
@@ -1734,11 +1769,15 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                 } else {
                     XScale xs;
                     xs.F = 0;
-                    o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, R, xs, a, runs, eflags, iters, dbg)
+                    o = s.mode == QM_DEC ? ch_resolve<QM_DEC>(sh, s, P, 1.0 / P, xs, a, runs, eflags, iters, dbg)
                                          : ch_resolve<QM_BIN>(sh, s, P, R, xs, a, runs, eflags, iters, dbg);
                 }
                 if (dbg && lane == 0) atomicAdd(&dbg[3 + o.kind], 1u);
                 CH_T(t1);
+#ifdef RL_STAMPS
+                cx[4 + (s.mode == QM_XDEC ? 1 : 0)] += t1 - t0;
+                cx[6 + (s.mode == QM_XDEC ? 1 : 0)] += 1;
+#endif
                 cyc[o.kind == CH_FULL ? 0 : 1] += t1 - t0;
                 t0 = t1;
                 if (o.kind == CH_FULL) {
@@ -1796,6 +1835,10 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         const uint32_t role = wave == 0 ? 0u : wave == 1 ? 1u : wave == (uint32_t)CH_LOADER ? 2u : 3u;
         if (role < 3)
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[24 + 4 * role + k], (uint32_t)(cyc[k] >> 4));
+        if (role == 1)
+            for (int k = 0; k < 4; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 2 ? cx[k] >> 4 : cx[k]));
+        if (role == 0)
+            for (int k = 4; k < 8; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 6 ? cx[k] >> 4 : cx[k]));
     }
 #endif
     if (tid == 0) {

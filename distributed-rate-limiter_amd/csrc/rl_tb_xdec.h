@@ -97,13 +97,17 @@ __device__ inline double xp10_inv(int k) {   // inexact beyond k = 0: only ever 
 // P[k] = 10^(13 - F - k) (all exact doubles; wave-uniform)
 struct XScale {
     double P[5];
+    double R[5];   // RN(1 / P[k]) (div_p10)
     int32_t F;
 };
 __device__ inline XScale xscale(int32_t F) {
     XScale s;
     s.F = F;
 #pragma unroll
-    for (int k = 0; k < 5; k++) s.P[k] = rlq::pow10_exact(13 - F - k);
+    for (int k = 0; k < 5; k++) {
+        s.P[k] = rlq::pow10_exact(13 - F - k);
+        s.R[k] = 1.0 / s.P[k];
+    }
     return s;
 }
 __device__ inline double xpick(const XScale& s, int k) {
@@ -113,6 +117,14 @@ __device__ inline double xpick(const XScale& s, int k) {
     p = k == 3 ? s.P[3] : p;
     p = k == 4 ? s.P[4] : p;
     return p;
+}
+__device__ inline double xpick_r(const XScale& s, int k) {
+    double r = s.R[0];
+    r = k == 1 ? s.R[1] : r;
+    r = k == 2 ? s.R[2] : r;
+    r = k == 3 ? s.R[3] : r;
+    r = k == 4 ? s.R[4] : r;
+    return r;
 }
 
 // One Redis-7 script step (tokenbucket.go:32-48) on a state X of a window with
@@ -136,8 +148,8 @@ __device__ __attribute__((always_inline)) inline bool xstep(int64_t X, const XSc
     const double Dd = rint((double)X * xp10_inv(kin));
     Xin = (int64_t)Dd * xp10_i(kin);
     // strtod("D e(E-13)"): |D| < 2^47 and the decade's scale is an exact power
-    // of ten, so one correctly rounded division is strtod (Clinger)
-    const double T = Dd / xpick(xs, kin);
+    // of ten, so one correctly rounded division is strtod (Clinger): div_p10
+    const double T = div_p10(Dd, xpick(xs, kin), xpick_r(xs, kin));
     const double sum = T + add;
     tokens = sum;
     up = false;
