@@ -468,7 +468,8 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "near_setup_x16": int(dbgw[39]) * 16,
                           # stamps build: producer 0's cycles on one-decade / multi-decade windows and their
                           # counts, then the chain's resolve cycles and counts the same way
-                          "split_x16": [int(dbgw[70 + k]) * (16 if k in (0, 1, 4, 5) else 1) for k in range(8)],
+                          "split_x16": [int(dbgw[70 + k]) * (16 if k in (0, 1, 4, 5) else 1) for k in range(8)]
+                          + [int(dbgw[80]) * 16, int(dbgw[81]) * 16],
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)

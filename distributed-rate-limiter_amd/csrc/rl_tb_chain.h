@@ -330,15 +330,18 @@ __device__ inline double round_scaled_Pd(double x, double P, bool& ge_lo) {
 }
 
 // x / P correctly rounded (as IEEE division) for an integer-valued |x| < 2^47,
-// P = 10^k (1 <= k <= 22, exact) and R = RN(1/P), in five dependent
-// operations instead of the division's eleven.  q1 = q0 + r R corrects the
-// product q0 = RN(x R) to within 1/2 ulp + 2^-51 ulp of x/P; the residual
-// r1 = x - q1 P is then exact (|r1| <= 0.51 ulp(q1) P < 2^53 units of
-// ulp(q1) ulp(P), as every 10^k has a mantissa below 2), and q1 + r1 R is
-// within 2^-54 ulp of x/P.  x/P = x / (2^k 5^k) with x an integer below
-// 2^47 is never a rounding midpoint and lies at least ulp / (2 5^k) >=
-// 2.1e-16 ulp from one (k <= 22), so the final rounding is RN(x/P).
-// Checked against IEEE division on 1.4e9 random (x, k): scripts/div_p10_check.c.
+// P = 10^k (1 <= k <= 22, exact) and R within 2^-52 relative of 1/P (RN(1/P),
+// or RN(1/10^j) times an exact 10^(j-k), rounded), in five dependent
+// operations instead of the division's eleven.  q0 = RN(x R) is within 3 ulp
+// of x/P and q1 = q0 + r R (r = x - q0 P, one rounding) within 1/2 ulp +
+// 1e-15 ulp; the residual r1 = x - q1 P is then exact (|r1| <= 0.51 ulp(q1) P
+// < 2^53 units of ulp(q1) ulp(P), as every 10^k has a mantissa below 2), and
+// q1 + r1 R is within 0.51 ulp 2^-52 = 1.1e-16 ulp of x/P.  x/P = x /
+// (2^k 5^k) with x an integer below 2^47 is never a rounding midpoint and lies
+// at least ulp / (2 5^k) >= 2.1e-16 ulp from one (k <= 22), so the final
+// rounding is RN(x/P).
+// Checked against IEEE division on 1.3e9 random (x, k), with both reciprocals:
+// scripts/div_p10_check.c.
 __device__ __attribute__((always_inline)) inline double div_p10(double x, double P, double R) {
     const double q0 = x * R;
     const double q1 = __builtin_fma(__builtin_fma(-q0, P, x), R, q0);
@@ -906,6 +909,8 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
         atomicAdd(&dbg[36], (uint32_t)((__builtin_amdgcn_s_memtime() - t_in) >> 4));
         atomicAdd(&dbg[37], ne);
         atomicAdd(&dbg[38], iters - it_in);
+        // [80]: the multi-decade windows' share of [36]
+        if (MODE == QM_XDEC) atomicAdd(&dbg[80], (uint32_t)((__builtin_amdgcn_s_memtime() - t_in) >> 4));
     }
 #endif
 
@@ -988,6 +993,7 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
             if (dbg && lane == 0 && s.hot) {   // [7] cycles / 16, [11] passes of the hot chain's exact tiles
                 atomicAdd(&dbg[7], (uint32_t)((__builtin_amdgcn_s_memtime() - t_ex) >> 4));
                 atomicAdd(&dbg[11], iters - it_ex);
+                if (MODE == QM_XDEC) atomicAdd(&dbg[81], (uint32_t)((__builtin_amdgcn_s_memtime() - t_ex) >> 4));
             }
 #endif
             if (brk > clen) {       // (never) give up on the window: one exact serial step

@@ -94,38 +94,28 @@ __device__ inline double xp10_inv(int k) {   // inexact beyond k = 0: only ever 
 }
 
 // A window's scale: PF = 10^(13 - F) and the scale of each of its decades,
-// P[k] = 10^(13 - F - k) (all exact doubles; wave-uniform)
+// P[k] = 10^(13 - F - k) (all exact doubles; wave-uniform).  A lane's decade
+// scale is computed, not indexed: P[k] = P4 10^(4 - k) exactly, and its
+// reciprocal R0 10^k, within 2^-52 of 1 / P[k] (div_p10's bound).  An indexed
+// pick from the array made the compiler keep it in scratch memory inside the
+// out-of-line multi-decade resolve: four dependent scratch loads per near pass.
 struct XScale {
     double P[5];
-    double R[5];   // RN(1 / P[k]) (div_p10)
+    double P4;     // P[4]
+    double R0;     // RN(1 / P[0])
     int32_t F;
 };
 __device__ inline XScale xscale(int32_t F) {
     XScale s;
     s.F = F;
 #pragma unroll
-    for (int k = 0; k < 5; k++) {
-        s.P[k] = rlq::pow10_exact(13 - F - k);
-        s.R[k] = 1.0 / s.P[k];
-    }
+    for (int k = 0; k < 5; k++) s.P[k] = rlq::pow10_exact(13 - F - k);
+    s.P4 = s.P[4];
+    s.R0 = 1.0 / s.P[0];
     return s;
 }
-__device__ inline double xpick(const XScale& s, int k) {
-    double p = s.P[0];
-    p = k == 1 ? s.P[1] : p;
-    p = k == 2 ? s.P[2] : p;
-    p = k == 3 ? s.P[3] : p;
-    p = k == 4 ? s.P[4] : p;
-    return p;
-}
-__device__ inline double xpick_r(const XScale& s, int k) {
-    double r = s.R[0];
-    r = k == 1 ? s.R[1] : r;
-    r = k == 2 ? s.R[2] : r;
-    r = k == 3 ? s.R[3] : r;
-    r = k == 4 ? s.R[4] : r;
-    return r;
-}
+__device__ inline double xpick(const XScale& s, int k) { return s.P4 * xp10_d(4 - k); }
+__device__ inline double xpick_r(const XScale& s, int k) { return s.R0 * xp10_d(k); }
 
 // One Redis-7 script step (tokenbucket.go:32-48) on a state X of a window with
 // floor F: strtod of the stored digits, the sum, %.14g of the result.  True

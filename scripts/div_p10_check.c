@@ -42,6 +42,31 @@ int main(int argc, char** argv) {
             }
         }
     }
+    /* the multi-decade windows' reciprocals: RN(10^-e0) times an exact 10^k
+     * (k <= 4), rounded -- within 2^-52 of 1 / 10^(e0 - k) */
+    for (int e0 = 5; e0 <= 22; e0++) {
+        double Pe = 1.0, Re;
+        for (int i = 0; i < e0; i++) Pe *= 10.0;
+        Re = 1.0 / Pe;
+        double t = 1.0;
+        for (int k = 0; k <= 4 && e0 - k >= 1; k++, t *= 10.0) {
+            double Pk = 1.0;
+            for (int i = 0; i < e0 - k; i++) Pk *= 10.0;
+            const double R = Re * t;
+            for (long i = 0; i < n / 8; i++) {
+                const uint64_t r = xs();
+                double x = (i & 1) ? (double)(10000000000000LL + (int64_t)(r % 90000000000000ull))
+                                   : (double)(r % 140737488355328ull);
+                if (i & 2) x = -x;
+                const double a = div_p10(x, Pk, R), b = x / Pk;
+                tot++;
+                if (a != b || signbit(a) != signbit(b)) {
+                    if (bad < 10) printf("e0=%d k=%d x=%.17g got %.17g want %.17g\n", e0, k, x, a, b);
+                    bad++;
+                }
+            }
+        }
+    }
     printf("div_p10: %ld cases, %ld mismatches\n", tot, bad);
     return bad != 0;
 }
