@@ -814,8 +814,7 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
                 const bool fl = rs && !brk;
                 const int64_t incl = seg_incl_scan_i64(fl, (v && !brk) ? d64 : 0, (int64_t)cbo);
                 outv = (int32_t)incl;
-                int32_t en = (int32_t)__shfl_up(outv, 1, 64);   // the guess: the offset after the lane before
-                if (lane == 0) en = cbo;
+                const int32_t en = wave_prev_i32(outv, cbo);    // the guess: the offset after the lane before
                 iters++;
                 if (it + 1 < CH_UNCHECKED) {
                     est = en;

@@ -142,53 +142,81 @@ __device__ __attribute__((always_inline)) inline bool xstep(int64_t X, const XSc
     const double T = div_p10(Dd, xpick(xs, kin), xpick_r(xs, kin));
     const double sum = T + add;
     tokens = sum;
-    up = false;
-    if (!(sum < th)) return false;
-    const double a = sum < 0.0 ? -sum : sum;
-    if (a == 0.0) {                              // tostring(0) == "0"
-        Xn = 0;
-        return true;
-    }
     // %.14g's decade on the exact scaled value (as tb_dec_step), starting at
-    // the decade the window's scale suggests
+    // the decade the window's scale suggests; a second decade only when the
+    // first misses (a wave-uniform branch: the near passes and exact tiles
+    // step every lane, so the common path carries no divergent branches)
+    const double a = sum < 0.0 ? -sum : sum;
     int k = xk_of_d(a * xs.P[0]);
-#pragma unroll
-    for (int g = 0; g < 2; g++) {
-        const double P = xpick(xs, k);
-        const double p = a * P, err = __builtin_fma(a, P, -p);     // a*P == p + err exactly
-        const bool lo_ok = (p > 1e13) | ((p == 1e13) & (err >= 0.0));
-        const bool hi_ok = (p < 1e14) | ((p == 1e14) & (err < 0.0));
-        if (lo_ok & hi_ok) {
-            double d = rint(p);                  // RNE of p; the exact product decides a tie of p
-            const double h = p - d;
-            d += ((h == 0.5) & (err > 0.0)) ? 1.0 : 0.0;
-            d -= ((h == -0.5) & (err < 0.0)) ? 1.0 : 0.0;
-            if (d == 1e14) {                     // rounding carried into the next decade
-                d = 1e13;
-                k += 1;
-                if (k > 4) return false;
-            }
-            const int64_t v = (int64_t)d * xp10_i(k);
-            Xn = sum < 0.0 ? -v : v;
-            up = X != 0 && k > kin;
-            return true;
-        }
-        k += lo_ok ? 1 : -1;
-        if (k < 0 || k > 4) return false;        // outside the window's decades
+    double P = xpick(xs, k);
+    double p = a * P, err = __builtin_fma(a, P, -p);     // a*P == p + err exactly
+    bool lo_ok = (p > 1e13) | ((p == 1e13) & (err >= 0.0));
+    bool hi_ok = (p < 1e14) | ((p == 1e14) & (err < 0.0));
+    bool kin_range = true;
+    if (__ballot(!(lo_ok & hi_ok)) != 0ull) {
+        const bool again = !(lo_ok & hi_ok);
+        const int k2 = k + (lo_ok ? 1 : -1);
+        kin_range = !again || (k2 >= 0 && k2 <= 4);      // outside the window's decades: not this regime
+        k = again ? k2 : k;
+        P = xpick(xs, k);
+        const double p2 = a * P, e2 = __builtin_fma(a, P, -p2);
+        p = again ? p2 : p;
+        err = again ? e2 : err;
+        lo_ok = (p > 1e13) | ((p == 1e13) & (err >= 0.0));
+        hi_ok = (p < 1e14) | ((p == 1e14) & (err < 0.0));
     }
-    return false;
+    // RNE of p; the exact product decides a tie of p
+    double d = rint(p);
+    const double h = p - d;
+    d += ((h == 0.5) & (err > 0.0)) ? 1.0 : ((h == -0.5) & (err < 0.0)) ? -1.0 : 0.0;
+    const bool carry = d == 1e14;                        // rounding carried into the next decade
+    d = carry ? 1e13 : d;
+    k += carry ? 1 : 0;
+    const int64_t v = (int64_t)d * xp10_i(k);
+    const bool zero = a == 0.0;                          // tostring(0) == "0"
+    const bool ok = (sum < th) && (zero || (kin_range && lo_ok && hi_ok && k <= 4));
+    Xn = !ok ? Xn : zero ? 0 : (sum < 0.0 ? -v : v);
+    up = ok && !zero && X != 0 && k > kin;
+    return ok;
 }
 
 // inclusive segmented scan over the wave: a lane with f set starts a segment
 // with its own v; lanes before the first segment add to base
+// (S, the scan of the other lanes' v, plus T, the offset of the lane's
+// segment: v - S at its start lane, base before any; T travels forward by the
+// DPP scan steps of wave_incl_scan_i64, a segment start keeping its own -- no
+// LDS round trips, where lane-indexed shuffles cost four ds_bpermute)
+template <int CTRL, int RM>
+__device__ inline int64_t dpp_i64(int64_t v, int64_t old) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)old, (int)(uint32_t)v, CTRL, RM, 0xf,
+                                                              false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)((uint64_t)old >> 32),
+                                                              (int)(uint32_t)((uint64_t)v >> 32), CTRL, RM, 0xf, false);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <int CTRL, int RM>
+__device__ inline void seg_step(int64_t& T, uint32_t& h) {
+    const uint32_t nh = dpp32<CTRL, RM>(h, 0u);
+    const int64_t nT = dpp_i64<CTRL, RM>(T, 0);
+    T = (h == 0u && nh != 0u) ? nT : T;
+    h |= nh;
+}
 __device__ inline int64_t seg_incl_scan_i64(bool f, int64_t v, int64_t base) {
-    const uint32_t lane = threadIdx.x & 63;
     const int64_t S = wave_incl_scan_i64(f ? 0 : v);
-    const uint32_t li = wave_scan_u32(f ? lane + 1u : 0u, 0u, [](uint32_t x, uint32_t y) { return x > y ? x : y; });
-    const int src = li ? (int)li - 1 : 0;
-    const int64_t rv = __shfl(v, src, 64);
-    const int64_t Sj = __shfl(S, src, 64);
-    return li ? rv + (S - Sj) : base + S;
+    int64_t T = f ? v - S : base;
+    uint32_t h = f ? 1u : 0u;
+    seg_step<0x111, 0xf>(T, h);   // row_shr:1
+    seg_step<0x112, 0xf>(T, h);   // row_shr:2
+    seg_step<0x114, 0xf>(T, h);   // row_shr:4
+    seg_step<0x118, 0xf>(T, h);   // row_shr:8
+    seg_step<0x142, 0xa>(T, h);   // row_bcast:15 -> rows 1, 3
+    seg_step<0x143, 0xc>(T, h);   // row_bcast:31 -> rows 2, 3
+    return T + S;
+}
+// the value of the lane before (lane 0: first) -- DPP wave_shr:1
+__device__ inline int64_t wave_prev_i64(int64_t v, int64_t first) { return dpp_i64<0x138, 0xf>(v, first); }
+__device__ inline int32_t wave_prev_i32(int32_t v, int32_t first) {
+    return (int32_t)dpp32<0x138, 0xf>((uint32_t)v, (uint32_t)first);
 }
 
 // inclusive wave scan of doubles (DPP, as wave_incl_scan_i64)
@@ -271,8 +299,7 @@ __device__ __attribute__((always_inline)) inline uint32_t exact_span_x(const Src
         // changes from the state the lane really started from (its guess
         // rounded onto a state): independent of the guess for far steps
         const int64_t incl = seg_incl_scan_i64(rs, rs ? X : (brk ? 0 : X - X0e), X0);
-        int64_t nst = __shfl_up(incl, 1, 64);
-        if (lane == 0) nst = X0;
+        const int64_t nst = wave_prev_i64(incl, X0);
         const uint32_t fb = first_lane(__ballot(brk));
         const uint32_t fd = first_lane(__ballot(nv > 0 && nst != st));
         iters++;
