@@ -1275,7 +1275,8 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     // runs come from the chain only: a light replay leaves none to expand
     // (mixed: 24 + 7 us per batch off the finish stream)
     if (!light) {
-        if (e->profile == PROFILE_REDIS7) k_tb_expand_x<<<32, 256, GROUP_LDS, t>>>(B.runs, ps, pre, e->d_eflags);
+        // (a wave per multi-decade run: ~300 per configs[1] batch, 32 blocks took 43 us)
+        if (e->profile == PROFILE_REDIS7) k_tb_expand_x<<<128, 256, GROUP_LDS, t>>>(B.runs, ps, pre, e->d_eflags);
         k_tb_expand<<<(int)std::min<uint32_t>((m + 4 * CH_TILE - 1) / (4 * CH_TILE), 2048), 256, GROUP_LDS, t>>>(
             m, B.runs, e->profile, ps, pre, e->d_eflags);
     }

@@ -13,6 +13,9 @@ for f in sorted(glob.glob(f"gpurun_out/{tag}_*.out"), key=os.path.getmtime):
         print(f"{name:24s} {tail[0][:100]}")
         continue
     d = json.loads(lines[-1])
+    if "value" not in d or "ms_per_step" not in d:
+        print(f"{name:24s} (no decisions/s line)")
+        continue
     rf = d.get("roofline", {})
     rd = d.get("replay_detail", {})
     print(f"{name:24s} {d['value']:.4e}  step {d['ms_per_step']*1e3:7.1f} us  replay {rf.get('launch_ms', 0)*1e3:7.1f} us"
