@@ -540,13 +540,10 @@ __global__ __launch_bounds__(RT_BLOCK) void k_bm_merge(uint32_t level, uint32_t 
     }
 }
 
-// Four consecutive requests per thread: their slots in one 16-byte load,
-// the four result records' loads issued before any is used, the decisions
-// stored as one 32-bit word and each other field as two 16-byte stores.  A
-// thread per request (round 4) left one dependent slot -> record chain in
-// flight per thread and stored decisions byte by byte: 64 us per 1M-request
-// step at world 1 (profiles/r4rt_routed_vs_local_mixed.md).
-constexpr uint32_t UNPACK_R = 4;
+// Results into the caller's order, one request per thread.  In a routed step
+// its kernel-trace time (64-67 us per 1M requests) is contention with the
+// replay and the next batch's grouping running beside it: alone it takes
+// 10 us (5.9 TB/s of its 61 bytes per request; profiles/r5m_route_unpack.txt).
 __device__ inline void unpack_one(uint32_t s, const rl_route_res* __restrict__ back, uint32_t& d, int64_t& rm,
                                   int64_t& rt, int64_t& rs) {
     if (s == 0xffffffffu) {   // dropped at the sender: never executed
@@ -565,42 +562,6 @@ __global__ __launch_bounds__(RT_BLOCK) void k_route_unpack(uint32_t m, const uin
                                                            uint8_t* __restrict__ dec, int64_t* __restrict__ rem,
                                                            int64_t* __restrict__ retry,
                                                            int64_t* __restrict__ reset) {
-    const uint32_t nq = m / UNPACK_R;   // full quads
-    for (uint32_t qd = blockIdx.x * RT_BLOCK + threadIdx.x; qd < nq; qd += gridDim.x * RT_BLOCK) {
-        const uint32_t i = qd * UNPACK_R;
-        const uint4 sl = *reinterpret_cast<const uint4*>(slot + i);
-        uint32_t d[UNPACK_R];
-        int64_t rm[UNPACK_R], rt[UNPACK_R], rs[UNPACK_R];
-        unpack_one(sl.x, back, d[0], rm[0], rt[0], rs[0]);
-        unpack_one(sl.y, back, d[1], rm[1], rt[1], rs[1]);
-        unpack_one(sl.z, back, d[2], rm[2], rt[2], rs[2]);
-        unpack_one(sl.w, back, d[3], rm[3], rt[3], rs[3]);
-        *reinterpret_cast<uint32_t*>(dec + i) = d[0] | (d[1] << 8) | (d[2] << 16) | (d[3] << 24);
-        *reinterpret_cast<longlong2*>(rem + i) = make_longlong2(rm[0], rm[1]);
-        *reinterpret_cast<longlong2*>(rem + i + 2) = make_longlong2(rm[2], rm[3]);
-        *reinterpret_cast<longlong2*>(retry + i) = make_longlong2(rt[0], rt[1]);
-        *reinterpret_cast<longlong2*>(retry + i + 2) = make_longlong2(rt[2], rt[3]);
-        *reinterpret_cast<longlong2*>(reset + i) = make_longlong2(rs[0], rs[1]);
-        *reinterpret_cast<longlong2*>(reset + i + 2) = make_longlong2(rs[2], rs[3]);
-    }
-    // the ragged tail (m % 4 requests), one per thread of the first block
-    if (blockIdx.x == 0 && threadIdx.x < m - nq * UNPACK_R) {
-        const uint32_t i = nq * UNPACK_R + threadIdx.x;
-        uint32_t d;
-        int64_t rm, rt, rs;
-        unpack_one(slot[i], back, d, rm, rt, rs);
-        dec[i] = (uint8_t)d;
-        rem[i] = rm;
-        retry[i] = rt;
-        reset[i] = rs;
-    }
-}
-
-__global__ __launch_bounds__(RT_BLOCK) void k_route_unpack_1(uint32_t m, const uint32_t* __restrict__ slot,
-                                                             const rl_route_res* __restrict__ back,
-                                                             uint8_t* __restrict__ dec, int64_t* __restrict__ rem,
-                                                             int64_t* __restrict__ retry,
-                                                             int64_t* __restrict__ reset) {
     for (uint32_t i = blockIdx.x * RT_BLOCK + threadIdx.x; i < m; i += gridDim.x * RT_BLOCK) {
         uint32_t d;
         int64_t rm, rt, rs;
@@ -768,15 +729,11 @@ extern "C" int rl_route_unpack(rl_router* r, size_t m, const uint32_t* slot, con
         return RL_EINVAL;
     if (!m) return RL_OK;
     (void)hipSetDevice(r->device);
-    // the vector loads and stores need 16-byte aligned arrays (torch and
-    // hipMalloc allocations are); anything else takes one request per thread
-    const bool al = ((uintptr_t)slot | (uintptr_t)decision | (uintptr_t)remaining | (uintptr_t)retry_after_ns |
-                     (uintptr_t)reset_at_ns) % 16 == 0 && ((uintptr_t)decision % 4 == 0);
-    if (al)
-        k_route_unpack<<<grid_for((m + UNPACK_R - 1) / UNPACK_R), RT_BLOCK, 0, (hipStream_t)stream>>>(
-            (uint32_t)m, slot, back, decision, remaining, retry_after_ns, reset_at_ns);
-    else
-        k_route_unpack_1<<<grid_for(m), RT_BLOCK, 0, (hipStream_t)stream>>>((uint32_t)m, slot, back, decision,
-                                                                           remaining, retry_after_ns, reset_at_ns);
+    // one request per thread: a wave reads 64 consecutive result records
+    // when the slots increase (each owner's results come back in its
+    // requests' order) -- 10 us per 1M requests in isolation, faster than
+    // four per thread (14.5 us; profiles/r5m_route_unpack.txt)
+    k_route_unpack<<<grid_for(m), RT_BLOCK, 0, (hipStream_t)stream>>>((uint32_t)m, slot, back, decision, remaining,
+                                                                     retry_after_ns, reset_at_ns);
     return hipGetLastError() == hipSuccess ? RL_OK : RL_EDEVICE;
 }

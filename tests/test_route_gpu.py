@@ -237,8 +237,8 @@ def test_route_merge_one_source_in_order_is_identity(rl):
 
 @pytest.mark.parametrize("m,shift", [(20_000, 0), (20_003, 0), (20_001, 1)])
 def test_route_unpack_dropped_and_kept(rl, m, shift):
-    """four requests per thread (ragged tails too), and unaligned outputs
-    (shift: every array one element in) through the one-per-thread kernel"""
+    """dropped and kept requests, odd batch sizes and unaligned outputs
+    (shift: every array one element in)"""
     import torch
 
     import route_ops
