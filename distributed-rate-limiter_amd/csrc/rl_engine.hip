@@ -487,6 +487,7 @@ namespace {
 constexpr int NSTAGES = 5;
 constexpr uint32_t STAMP_RING = 256;
 constexpr int NSETS = 3;          // batch buffer sets: grouping b+1 | replay b | finish b-1
+constexpr uint32_t LIGHT_MIN_BATCH = 1u << 19;   // batches this large may take k_replay_light
 constexpr int GROUP_LDS = 4096;   // LDS floor of the grouping / finish kernels (see rl_engine::chain_pad)
 // A set's zeroed words.  The head (list counts, queues, diagnostics) is read
 // by the host after the batch (rl_engine_stats), so k_probe zeroes it when the
@@ -1240,8 +1241,11 @@ static int run_batch(rl_engine* e, uint32_t m, ReqArgs a, hipStream_t s, bool in
     const hipEvent_t ev_a = bound_ev ? ev[4] : nullptr, ev_b = bound_ev ? ev[5] : bind_done ? B.chain_done : nullptr;
     // no huge segment in the last replay seen: the light replay kernel
     // (k_replay_light; a huge segment that comes anyway is replayed exactly,
-    // as a heavy one, and flips the prediction back)
-    const bool light = e->light_ok && (e->force_light || *(volatile uint32_t*)e->h_huge == 0u);
+    // as a heavy one, and flips the prediction back).  Large batches only:
+    // a server's batches swing from small ones (no huge segment) to a large
+    // one after a stall, whose hot key the light kernel would replay as one
+    // wave -- an 8 ms batch at 1e7 QPS (profiles/r5z2_e2e.json window 13)
+    const bool light = e->light_ok && (e->force_light || (m >= LIGHT_MIN_BATCH && *(volatile uint32_t*)e->h_huge == 0u));
     e->stats.light_batches += light ? 1 : 0;
     const int lc = ncfg <= (uint32_t)MAX_LCFG ? 0 : 1;
     if (light)

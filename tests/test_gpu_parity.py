@@ -248,6 +248,38 @@ def test_sort_predicted_plan_and_misprediction(rl):
     assert pred == [0, 1, 1, 1, 0, 0, 1]        # batch 3 (hot) mispredicted: loc_sort_big
 
 
+def test_light_replay_and_misprediction(rl):
+    # after a large batch with no huge segment the engine launches the light
+    # replay kernel (k_replay_light: no chain) for the next large batch; one
+    # that brings a hot key anyway replays it exactly as a heavy segment (one
+    # wave) and flips the prediction back to the chain kernel.  Small batches
+    # always take the chain kernel.  Every batch against the oracle.
+    configs = CONFIG_SETS["mixed"]
+    rng = np.random.default_rng(11)
+    batches, t = [], T0
+    for kind, m in [("u", 600_000), ("hot", 600_000), ("hot", 600_000), ("u", 100_000), ("u", 600_000)]:
+        key = rng.integers(1000, 3_000_000, m).astype(np.uint64)
+        if kind == "hot":
+            r = rng.random(m)
+            key[r < 0.3] = 15                      # a token-bucket key (15 % 15 == 0): 180k requests
+            key[(r >= 0.3) & (r < 0.4)] = 20       # and 60k of a sliding-window key
+        ts = t + np.cumsum(rng.integers(0, 40_000, m)).astype(np.int64)
+        t = int(ts[-1])
+        n = rng.choice([1, 1, 2], m).astype(np.int64)
+        batches.append((key, ts, n, (key % len(configs)).astype(np.uint32), None))
+    eng = make_engine(rl, 0, tb=1 << 22, win=1 << 22)
+    sim = oracle.OracleSim(0)
+    for a, L, W in configs:
+        assert eng.register(a, L, W) == sim.add_config(a, L, W)
+    light = []
+    for i, (key, ts, n, cfg, sms) in enumerate(batches):
+        before = eng.stats().light_batches
+        res = eng.decide(key, ts, n, cfg, sms)
+        assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
+        light.append(int(eng.stats().light_batches - before))
+    assert light == [0, 1, 0, 0, 1]
+
+
 def test_single_hot_key_full_batch(rl):
     # the bench's diagnostic workload: one key carries the whole 1M batch
     g = traces.TokenBucketZipf(nkeys=1, batch=1_000_000)
