@@ -2,7 +2,7 @@
 # One GPU call's worth of named measurement steps (replaces round 4's one-off
 # scripts/steps_r4*.txt files).  Usage, on the gpurun box:
 #
-#   bash scripts/steps.sh TAG SET [SET ...] [-- EXTRA_STEPS_FILE]
+#   bash scripts/steps.sh TAG SET [SET ...] [-- EXTRA_STEPS_FILE [PREFIX]]
 #
 # Each step runs under its own time limit through scripts/gpusteps.sh (output
 # in gpurun_out/TAG_<step>.out/.err); a step that times out, aborts or faults
@@ -21,7 +21,9 @@
 #   prof    rocprofv3 kernel trace + FETCH_SIZE / WRITE_SIZE passes of the
 #           driver's command (scripts/profile.sh, TAG_zipf)
 #   proft   the kernel trace only
-# EXTRA_STEPS_FILE: further "<name> <seconds> <command>" lines (ad-hoc A/Bs).
+# EXTRA_STEPS_FILE [PREFIX]: further "<name> <seconds> <command>" lines (ad-hoc
+# A/Bs; scripts/ab_r5.txt holds this round's), only those whose name starts
+# with PREFIX when one is given.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1
@@ -52,7 +54,8 @@ while [ $# -gt 0 ]; do
     grpc) echo "${TAG}_grpc 400 python -u bench.py --grpc" ;;
     prof) echo "${TAG}_prof 700 TAG=${TAG}_zipf BARGS=\"--steps 20 --warmup 5\" bash scripts/profile.sh" ;;
     proft) echo "${TAG}_proft 300 TAG=${TAG}_zipf NO_PMC=1 BARGS=\"--steps 20 --warmup 5\" bash scripts/profile.sh" ;;
-    --) shift; cat "$1" ;;
+    --) shift
+        if [ $# -ge 2 ]; then grep -E "^$2" "$1"; shift; else cat "$1"; fi ;;
     *) echo "unknown set $1" >&2; exit 2 ;;
     esac
     shift
