@@ -114,6 +114,7 @@ static_assert(RING >= 3 * CH_W + 256, "the ring must hold three windows");
 
 struct ChTile {
     int64_t S;          // nominal sum of the tile's increments r
+    double Sd;          // S as a double (the producers' state bound sums it every round)
     double ymin;        // min over steps of (th * P * CH_YSCALE - inclusive nominal prefix)
     double cmax, cmin;  // max / min inclusive nominal prefix
     double dmax;        // the near band assumed every state of the tile is <= dmax
@@ -577,6 +578,7 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     if (lane == 63) {
         ChTile& T = sh.tile[buf][t];
         T.S = incl;
+        T.Sd = (double)incl;
         T.ymin = ymin_t;
         T.cmax = cmax_t;
         T.cmin = cmin_t;
@@ -1695,14 +1697,13 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                         // climb ~4e-3 tokens per window under a +-2e-3 sawtooth of
                         // last_refill's rounding, which broke the bound in ~40 % of
                         // its tiles -- each then replayed exactly
-                        int64_t G = 0;
-                        double pk = 0.0;
+                        double G = 0.0, pk = 0.0;
 #pragma unroll
                         for (int t = 0; t < CH_NP; t++) {
-                            pk = fmax(pk, (double)G + sh.tile[s.cbuf][t].cmax);
-                            G += sh.tile[s.cbuf][t].S;
+                            pk = fmax(pk, G + sh.tile[s.cbuf][t].cmax);
+                            G += sh.tile[s.cbuf][t].Sd;   // exact: |G| < 2^53
                         }
-                        const double g = (double)(G > 0 ? G : 0);
+                        const double g = G > 0.0 ? G : 0.0;
                         dmax = fmin(dmax, (double)s.D + g + fmax(1.25 * g, 1.5 * pk) + 0x1p21);
                     }
                 } else {

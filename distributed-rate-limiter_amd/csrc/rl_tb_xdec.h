@@ -504,6 +504,7 @@ __device__ __attribute__((always_inline)) inline void ch_produce_x(ChainShared& 
         sh.ne_kind[buf][t] = ((uint64_t)khi << 32) | klo;
         ChTile& T = sh.tile[buf][t];
         T.S = incl;
+        T.Sd = (double)incl;
         T.ymin = ymin_t;
         T.cmax = vt * PF;
         T.cmin = dev_t;
