@@ -513,8 +513,11 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     // (|D| + |D'|) 2^-53 (which the binary mode keeps)
     double band = 2.0 * dmax * 0x1.0000001p-53;
     if (MODE == QM_DEC) {
-        int e;
-        (void)frexp(dmax / P * 0x1.0000001p+0, &e);
+        // e: the binade of dmax / P, from the operands' binades and mantissas
+        // (no division); the margin only ever picks the binade above
+        int ed, ep;
+        const double md = frexp(dmax, &ed), mp = frexp(P, &ep);
+        const int e = ed - ep + (md * 0x1.00001p+0 >= mp ? 1 : 0);
         band = ldexp(P, e - 53) * 0x1.0000001p+0;
     }
     const double lim = 0.5 - (band + 0x1p-40);
@@ -522,14 +525,50 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     double add[K], th[K], cb[K];
     double cum = 0.0, ymin = __builtin_inf(), cmax = -__builtin_inf(), cmin = __builtin_inf();
     uint32_t nearm = 0, evq = NO_STOP;
+    // the lane's K adds and thresholds: whole 16-byte granules (the window's
+    // parity is wave-uniform: i0 = pfirst + an even offset), K / 2 or K / 2 + 1
+    // ds_read_b128 per array instead of K ds_read_b64
+    double ra[K], rt[K];
+    if constexpr (K % 2 == 0) {
+        const uint32_t g0 = i0 >> 1;
+        if ((i0 & 1u) == 0u) {
+#pragma unroll
+            for (int j = 0; j < K / 2; j++) {
+                const double2 a2 = sh.r_add[ring_slot(g0 + j)], t2 = sh.r_th[ring_slot(g0 + j)];
+                ra[2 * j] = a2.x;
+                ra[2 * j + 1] = a2.y;
+                rt[2 * j] = t2.x;
+                rt[2 * j + 1] = t2.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j <= K / 2; j++) {
+                const double2 a2 = sh.r_add[ring_slot(g0 + j)], t2 = sh.r_th[ring_slot(g0 + j)];
+                if (j > 0) {
+                    ra[2 * j - 1] = a2.x;
+                    rt[2 * j - 1] = t2.x;
+                }
+                if (j < K / 2) {
+                    ra[2 * j] = a2.y;
+                    rt[2 * j] = t2.y;
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            ra[q] = ring_add(sh, i0 + q);
+            rt[q] = ring_th(sh, i0 + q);
+        }
+    }
     // branch-free: every ring slot is readable (positions past the window
     // read stale slots, masked by v), and the bounds use v_max / v_min on
     // values that are never NaN (no canonicalization)
 #pragma unroll
     for (int q = 0; q < K; q++) {
         const bool v = (uint32_t)q < nv;
-        const double araw = ring_add(sh, i0 + q);
-        const double h = ring_th(sh, i0 + q);
+        const double araw = ra[q];
+        const double h = rt[q];
         const double a = v ? araw : 0.0;
         add[q] = a;
         th[q] = h;
