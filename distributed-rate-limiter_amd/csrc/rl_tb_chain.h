@@ -217,6 +217,31 @@ __device__ inline double wave_reduce_f64(double v, double ident, Op op) {
     v = op(v, dpp_f64<0x143, 0xc>(v, ident));
     return readlane_f64(v, 63);
 }
+// inclusive wave scan of doubles (DPP, as wave_incl_scan_i64)
+template <int CTRL, int RM>
+__device__ inline double dpp_addf_step(double v) {
+    return v + dpp_f64<CTRL, RM>(v, 0.0);
+}
+__device__ inline double wave_incl_scan_f64(double v) {
+    v = dpp_addf_step<0x111, 0xf>(v);
+    v = dpp_addf_step<0x112, 0xf>(v);
+    v = dpp_addf_step<0x114, 0xf>(v);
+    v = dpp_addf_step<0x118, 0xf>(v);
+    v = dpp_addf_step<0x142, 0xa>(v);
+    v = dpp_addf_step<0x143, 0xc>(v);
+    return v;
+}
+// the same reduction, left in lane 63 only (its caller reads it there)
+template <typename Op>
+__device__ inline double wave_fold_f64(double v, double ident, Op op) {
+    v = op(v, dpp_f64<0x111, 0xf>(v, ident));
+    v = op(v, dpp_f64<0x112, 0xf>(v, ident));
+    v = op(v, dpp_f64<0x114, 0xf>(v, ident));
+    v = op(v, dpp_f64<0x118, 0xf>(v, ident));
+    v = op(v, dpp_f64<0x142, 0xa>(v, ident));
+    v = op(v, dpp_f64<0x143, 0xc>(v, ident));
+    return v;
+}
 __device__ inline int64_t readfirstlane_i64(int64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
@@ -590,13 +615,24 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
         cmin = v ? mn : cmin;
         ymin = v ? ym : ymin;
     }
-    const int64_t Si = (int64_t)cum;
-    const int64_t incl = wave_incl_scan_i64(Si);
-    const double ex = (double)(incl - Si);
-    const double ymin_t = wave_reduce_f64(ymin - ex, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
-    const double cmax_t = wave_reduce_f64(ex + cmax, -__builtin_inf(), [](double x, double y) { return vmax_f64(x, y); });
-    const double cmin_t = wave_reduce_f64(ex + cmin, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
-    const uint32_t ev_t = wave_min_u32(evq != NO_STOP ? lane * K + evq : NO_STOP);
+    // the tile prefix: in doubles when every lane's sum is below 2^46 (the
+    // tile's then below 2^52: exact), else in int64
+    double ex, inclD;
+    if (__ballot(!(fabs(cum) < 0x1p46)) == 0ull) {
+        inclD = wave_incl_scan_f64(cum);
+        ex = inclD - cum;
+    } else {
+        const int64_t Si = (int64_t)cum;
+        const int64_t incl = wave_incl_scan_i64(Si);
+        ex = (double)(incl - Si);
+        inclD = (double)incl;
+    }
+    // the tile's bounds: lane 63 holds the reductions (no broadcast)
+    const double ymin_t = wave_fold_f64(ymin - ex, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
+    const double cmax_t = wave_fold_f64(ex + cmax, -__builtin_inf(), [](double x, double y) { return vmax_f64(x, y); });
+    const double cmin_t = wave_fold_f64(ex + cmin, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
+    const uint32_t ev_t = wave_scan_u32(evq != NO_STOP ? lane * K + evq : NO_STOP, 0xffffffffu,
+                                        [](uint32_t a, uint32_t b) { return a < b ? a : b; });
     const uint32_t ncnt = (uint32_t)__popc(nearm);
     const uint32_t ninc = wave_scan_u32(ncnt, 0u, [](uint32_t x, uint32_t y) { return x + y; });
     sh.ne_rank[buf][t][lane] = (uint16_t)(ninc - ncnt);
@@ -616,8 +652,8 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     }
     if (lane == 63) {
         ChTile& T = sh.tile[buf][t];
-        T.S = incl;
-        T.Sd = (double)incl;
+        T.S = (int64_t)inclD;
+        T.Sd = inclD;
         T.ymin = ymin_t;
         T.cmax = cmax_t;
         T.cmin = cmin_t;

@@ -219,20 +219,6 @@ __device__ inline int32_t wave_prev_i32(int32_t v, int32_t first) {
     return (int32_t)dpp32<0x138, 0xf>((uint32_t)v, (uint32_t)first);
 }
 
-// inclusive wave scan of doubles (DPP, as wave_incl_scan_i64)
-template <int CTRL, int RM>
-__device__ inline double dpp_addf_step(double v) {
-    return v + dpp_f64<CTRL, RM>(v, 0.0);
-}
-__device__ inline double wave_incl_scan_f64(double v) {
-    v = dpp_addf_step<0x111, 0xf>(v);
-    v = dpp_addf_step<0x112, 0xf>(v);
-    v = dpp_addf_step<0x114, 0xf>(v);
-    v = dpp_addf_step<0x118, 0xf>(v);
-    v = dpp_addf_step<0x142, 0xa>(v);
-    v = dpp_addf_step<0x143, 0xc>(v);
-    return v;
-}
 
 // Exact replay of [p, p + len) (len <= CH_TILE) from the exact state X0 of a
 // window with floor xs.F by one wave (the multi-decade exact_span): lane l
