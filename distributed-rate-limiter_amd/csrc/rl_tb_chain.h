@@ -515,6 +515,48 @@ __device__ __attribute__((always_inline)) inline uint32_t exact_span(const Src& 
 // ---------------------------------------------------------------------------
 // producers
 // ---------------------------------------------------------------------------
+// a lane's K consecutive adds and thresholds from the ring, positions i0 ..
+// i0 + K - 1, in whole 16-byte granules: K / 2 or K / 2 + 1 ds_read_b128 per
+// array instead of K ds_read_b64 (i0's parity must be wave-uniform: the
+// callers' i0 is a window start plus an even offset)
+__device__ __attribute__((always_inline)) inline void ring_read_k(const ChainShared& sh, uint32_t i0,
+                                                                 double (&ra)[CH_K], double (&rt)[CH_K]) {
+    constexpr int K = CH_K;
+    if constexpr (K % 2 == 0) {
+        const uint32_t g0 = i0 >> 1;
+        if ((i0 & 1u) == 0u) {
+#pragma unroll
+            for (int j = 0; j < K / 2; j++) {
+                const double2 a2 = sh.r_add[ring_slot(g0 + j)], t2 = sh.r_th[ring_slot(g0 + j)];
+                ra[2 * j] = a2.x;
+                ra[2 * j + 1] = a2.y;
+                rt[2 * j] = t2.x;
+                rt[2 * j + 1] = t2.y;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j <= K / 2; j++) {
+                const double2 a2 = sh.r_add[ring_slot(g0 + j)], t2 = sh.r_th[ring_slot(g0 + j)];
+                if (j > 0) {
+                    ra[2 * j - 1] = a2.x;
+                    rt[2 * j - 1] = t2.x;
+                }
+                if (j < K / 2) {
+                    ra[2 * j] = a2.y;
+                    rt[2 * j] = t2.y;
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            ra[q] = ring_add(sh, i0 + q);
+            rt[q] = ring_th(sh, i0 + q);
+        }
+    }
+}
+
+
 // Summary of tile t of the window [pfirst, pfirst + pcnt) at scale P, into
 // tile[buf][t], its near list and per-lane near ranks.  State-free except for
 // dmax, an estimated bound on the window's states that narrows the near band
@@ -550,42 +592,8 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     double add[K], th[K], cb[K];
     double cum = 0.0, ymin = __builtin_inf(), cmax = -__builtin_inf(), cmin = __builtin_inf();
     uint32_t nearm = 0, evq = NO_STOP;
-    // the lane's K adds and thresholds: whole 16-byte granules (the window's
-    // parity is wave-uniform: i0 = pfirst + an even offset), K / 2 or K / 2 + 1
-    // ds_read_b128 per array instead of K ds_read_b64
     double ra[K], rt[K];
-    if constexpr (K % 2 == 0) {
-        const uint32_t g0 = i0 >> 1;
-        if ((i0 & 1u) == 0u) {
-#pragma unroll
-            for (int j = 0; j < K / 2; j++) {
-                const double2 a2 = sh.r_add[ring_slot(g0 + j)], t2 = sh.r_th[ring_slot(g0 + j)];
-                ra[2 * j] = a2.x;
-                ra[2 * j + 1] = a2.y;
-                rt[2 * j] = t2.x;
-                rt[2 * j + 1] = t2.y;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j <= K / 2; j++) {
-                const double2 a2 = sh.r_add[ring_slot(g0 + j)], t2 = sh.r_th[ring_slot(g0 + j)];
-                if (j > 0) {
-                    ra[2 * j - 1] = a2.x;
-                    rt[2 * j - 1] = t2.x;
-                }
-                if (j < K / 2) {
-                    ra[2 * j] = a2.y;
-                    rt[2 * j] = t2.y;
-                }
-            }
-        }
-    } else {
-#pragma unroll
-        for (int q = 0; q < K; q++) {
-            ra[q] = ring_add(sh, i0 + q);
-            rt[q] = ring_th(sh, i0 + q);
-        }
-    }
+    ring_read_k(sh, i0, ra, rt);
     // branch-free: every ring slot is readable (positions past the window
     // read stale slots, masked by v), and the bounds use v_max / v_min on
     // values that are never NaN (no canonicalization)
@@ -678,34 +686,35 @@ __device__ __attribute__((always_inline)) inline ChSpec ch_predict(const ChainSh
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t nt = (s.ccnt + CH_TILE - 1) / CH_TILE;
     const bool tv = lane < nt;
+    // (a guess: nominal sums in doubles, exact below 2^53, and only a guess
+    // beyond -- the chain adopts the window only if its exact replay agrees)
     const ChTile T = sh.tile[s.cbuf][tv ? lane : 0u];
-    const int64_t Sl = tv ? T.S : 0;
-    const int64_t Dt = s.D + wave_incl_scan_i64(Sl) - Sl;          // nominal start of tile t
-    const double dD = (double)Dt;
+    const double Sl = tv ? T.Sd : 0.0;
+    const double dD = (double)s.D + (wave_incl_scan_f64(Sl) - Sl);   // nominal start of tile t
     const bool cand = tv && (T.ev != NO_STOP || !(dD + T.cmax < (double)DEC_HI) ||
                              !(dD + T.cmin >= (double)DEC_LO + 1.0) || !(dD + 3.0 < T.ymin));
     const uint64_t cm = __ballot(cand);
     if (!cm) return sp;
     const uint32_t c = first_lane(cm);
-    const int64_t Dc = readlane_i64(Dt, c);
+    const double Dc = readlane_f64(dD, c);
     const uint32_t p0 = s.cfirst + c * CH_TILE;
     const uint32_t clen = (s.ccnt - c * CH_TILE) < CH_TILE ? (s.ccnt - c * CH_TILE) : CH_TILE;
     const uint32_t off = lane * K;
     const uint32_t nv = off < clen ? ((clen - off) < (uint32_t)K ? (clen - off) : (uint32_t)K) : 0u;
     double add[K], th[K];
-    int64_t S = 0;
+    ring_read_k(sh, p0 + off, add, th);
+    double S = 0.0;
 #pragma unroll
     for (int q = 0; q < K; q++) {
         const bool v = (uint32_t)q < nv;
-        add[q] = v ? ring_add(sh, p0 + off + q) : 0.0;
-        th[q] = v ? ring_th(sh, p0 + off + q) : __builtin_inf();
+        add[q] = v ? add[q] : 0.0;
+        th[q] = v ? th[q] : __builtin_inf();
         const double pr = add[q] * P;
-        if (fabs(pr) < 0x1p49) S += (int64_t)rint(pr);
+        if (fabs(pr) < 0x1p49) S += rint(pr);
     }
-    const int64_t incl = wave_incl_scan_i64(S);
     // nominal states (integer digits, no %.14g step): an exit where the sum
     // reaches th (D + add P >= th P) or the next digits leave the decade
-    double D = (double)(Dc + incl - S);
+    double D = Dc + (wave_incl_scan_f64(S) - S);
     uint32_t bq = NO_STOP;
     double D_b = 0.0, a_b = 0.0, th_b = 0.0;
 #pragma unroll
