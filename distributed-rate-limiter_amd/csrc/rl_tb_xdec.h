@@ -327,10 +327,12 @@ __device__ __attribute__((always_inline)) inline XPlan ch_plan(const ChainShared
     for (int t = 0; t < CH_NP; t++) {
         pl.vt[t] = v;
         double s = 0.0, sp = 0.0;
+        double ra[K], rt[K];
+        ring_read_k(sh, first + (uint32_t)t * CH_TILE + lane * K, ra, rt);
 #pragma unroll
         for (int q = 0; q < K; q++) {
             const uint32_t o = (uint32_t)t * CH_TILE + lane * K + q;
-            const double ad = ring_add(sh, first + o);
+            const double ad = ra[q];
             const double x = (o < cnt && fabs(ad) < 1e300) ? ad : 0.0;
             s += x;
             sp += x > 0.0 ? x : 0.0;
@@ -391,12 +393,11 @@ __device__ __attribute__((always_inline)) inline void ch_produce_x(ChainShared& 
     double add[K], th[K], A[K];
     double SA = 0.0;
     uint32_t evq = NO_STOP;
+    ring_read_k(sh, i0, add, th);
 #pragma unroll
     for (int q = 0; q < K; q++) {
         const bool v = (uint32_t)q < nv;
-        const double ad = ring_add(sh, i0 + q);
-        add[q] = v ? ad : 0.0;
-        th[q] = ring_th(sh, i0 + q);
+        add[q] = v ? add[q] : 0.0;
         const double a2 = add[q] * PF;
         const bool ok = fabs(a2) < 0x1p62;                 // else NaN (expired key) or huge: a stop
         evq = (v && !ok && evq == NO_STOP) ? (uint32_t)q : evq;
