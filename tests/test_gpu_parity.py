@@ -168,7 +168,7 @@ def test_chain_regimes(rl, profile, kind):
     run_both(rl, profile, configs, split(_chain_trace(kind, seed), [50_000, 70_000]))
 
 
-def _random_config_trace(seed, alg, m):
+def _random_config_trace(seed, alg, m, nk=None):
     """Seeded random configurations (limit 1 .. 1e12 log-uniform, window 1 ms
     .. ~1 day) and a few hot keys whose gaps are drawn around each config's
     refill period (limit / window): the chain's decades, multi-decade windows,
@@ -181,7 +181,7 @@ def _random_config_trace(seed, alg, m):
         L = max(1, int(round(10 ** rng.uniform(0, 12))))
         W = int(round(10 ** rng.uniform(6, 13.9)))
         configs.append((a, L, W))
-    nk = int(rng.integers(1, 5))
+    nk = nk or int(rng.integers(1, 5))
     key = rng.integers(0, nk, m).astype(np.uint64)
     cfg = (key % 3).astype(np.uint32)
     period = np.array([W / L for _, L, W in configs])[cfg]          # ns per token
@@ -214,6 +214,19 @@ def test_chain_random_configs(rl, seed):
 def test_window_random_configs(rl, seed):
     configs, tr = _random_config_trace(800 + seed, 2 + seed % 2 if seed < 4 else 0, 90_000)
     run_both(rl, seed % 2, configs, split(tr, [30_000, 60_000]), tb=1 << 12, win=1 << 12)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_configs_many_keys(rl, seed, monkeypatch):
+    """The same random configurations over many keys: batches below the
+    single-workgroup limit (k_small), mid-size batches (the full launch
+    sequence, light segments) and batches of 2^19 and more with no hot key,
+    which after the first take the light replay kernel."""
+    monkeypatch.setenv("RL_SMALL_MAX", "4096")
+    configs, tr = _random_config_trace(900 + seed, 0, 1_300_000, nk=40_000 + 20_000 * seed)
+    eng, _ = run_both(rl, seed % 2, configs, split(tr, [3000, 4096, 90_000, 600_000, 602_904]),
+                      tb=1 << 17, win=1 << 17)
+    assert eng.stats().light_batches >= 1
 
 
 @pytest.mark.parametrize("counts", [
