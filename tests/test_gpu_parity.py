@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 import traces
-from tracegen import CONFIG_SETS, T0, NS, random_trace, skewed_trace
+from tracegen import CONFIG_SETS, T0, NS, random_config_trace, random_trace, skewed_trace
 
 pytestmark = pytest.mark.gpu
 
@@ -168,51 +168,15 @@ def test_chain_regimes(rl, profile, kind):
     run_both(rl, profile, configs, split(_chain_trace(kind, seed), [50_000, 70_000]))
 
 
-def _random_config_trace(seed, alg, m, nk=None):
-    """Seeded random configurations (limit 1 .. 1e12 log-uniform, window 1 ms
-    .. ~1 day) and a few hot keys whose gaps are drawn around each config's
-    refill period (limit / window): the chain's decades, multi-decade windows,
-    allows, clamps and expiries at scales the fixed configs above never reach;
-    for the window algorithms, runs that cross window starts at every scale."""
-    rng = np.random.default_rng(seed)
-    configs = []
-    for _ in range(3):
-        a = alg if alg else int(rng.integers(1, 4))
-        L = max(1, int(round(10 ** rng.uniform(0, 12))))
-        W = int(round(10 ** rng.uniform(6, 13.9)))
-        configs.append((a, L, W))
-    nk = nk or int(rng.integers(1, 5))
-    key = rng.integers(0, nk, m).astype(np.uint64)
-    cfg = (key % 3).astype(np.uint32)
-    period = np.array([W / L for _, L, W in configs])[cfg]          # ns per token
-    lim = np.array([L for _, L, _ in configs])[cfg]
-    # per phase of 3000 requests: a request takes a fraction f of the bucket and
-    # arrivals per refilled token drift around 1 -- long denial stretches (deep
-    # near-empty balances, decade crossings), refills to the cap, and allows
-    ph = m // 3000 + 1
-    f = np.repeat(10 ** rng.uniform(-6, -1, ph), 3000)[:m]
-    scale = np.repeat(10 ** rng.uniform(-1.5, 1, ph), 3000)[:m]
-    n = np.maximum(1, np.rint(lim * f)).astype(np.int64) * rng.choice([1, 1, 1, 2], m)
-    gaps = np.rint(rng.exponential(1.0, m) * period * n * scale / nk)
-    gaps[rng.random(m) < 0.05] = 0
-    gaps = np.minimum(gaps, 10 ** 12)                                # ts stays far from int64 overflow
-    r = rng.random(m)
-    big = r < 0.01
-    n[big] = np.maximum(1, (lim[big] * rng.random(int(big.sum())) * 1.3).astype(np.int64))
-    n[r > 0.999] = 1 << 62
-    ts = T0 + np.cumsum(gaps).astype(np.int64)
-    return configs, (key, ts, n, cfg, None)
-
-
 @pytest.mark.parametrize("seed", range(16))
 def test_chain_random_configs(rl, seed):
-    configs, tr = _random_config_trace(700 + seed, 1, 90_000)
+    configs, tr = random_config_trace(700 + seed, 1, 90_000)
     run_both(rl, seed % 2, configs, split(tr, [30_000, 60_000]), tb=1 << 12, win=1 << 12)
 
 
 @pytest.mark.parametrize("seed", range(8))
 def test_window_random_configs(rl, seed):
-    configs, tr = _random_config_trace(800 + seed, 2 + seed % 2 if seed < 4 else 0, 90_000)
+    configs, tr = random_config_trace(800 + seed, 2 + seed % 2 if seed < 4 else 0, 90_000)
     run_both(rl, seed % 2, configs, split(tr, [30_000, 60_000]), tb=1 << 12, win=1 << 12)
 
 
@@ -223,7 +187,7 @@ def test_random_configs_many_keys(rl, seed, monkeypatch):
     sequence, light segments) and batches of 2^19 and more with no hot key,
     which after the first take the light replay kernel."""
     monkeypatch.setenv("RL_SMALL_MAX", "4096")
-    configs, tr = _random_config_trace(900 + seed, 0, 1_300_000, nk=40_000 + 20_000 * seed)
+    configs, tr = random_config_trace(900 + seed, 0, 1_300_000, nk=40_000 + 20_000 * seed)
     eng, _ = run_both(rl, seed % 2, configs, split(tr, [3000, 4096, 90_000, 600_000, 602_904]),
                       tb=1 << 17, win=1 << 17)
     assert eng.stats().light_batches >= 1

@@ -91,7 +91,7 @@ def test_lua_tostring_roundtrip(lib):
 
 # --- C oracle vs independent Python restatement --------------------------------
 
-from tracegen import CONFIG_SETS, random_trace, skewed_trace  # noqa: E402
+from tracegen import CONFIG_SETS, random_config_trace, random_trace, skewed_trace  # noqa: E402
 
 
 @pytest.mark.parametrize("profile", [0, 1])
@@ -109,6 +109,25 @@ def test_c_vs_python(lib, profile, kind, ff):
     dec, rem, retry, reset, tok = c.decide(keys, ts, n, cfg, sms)
     for i in range(len(keys)):
         d = p.decide(int(keys[i]), int(ts[i]), int(n[i]), int(cfg[i]), None if sms is None else int(sms[i]))
+        got = (int(dec[i]), int(rem[i]), int(retry[i]), int(reset[i]))
+        assert got == d[:4], (i, got, d)
+        if configs[cfg[i]][0] == 1 and d[0] in (0, 1):
+            assert tok[i] == d[4] or (math.isnan(tok[i]) and math.isnan(d[4]))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_c_vs_python_random_configs(lib, seed):
+    # the GPU parity suite's random configurations (limits 1 .. 1e12, windows
+    # 1 ms .. a day): the two restatements agree at those scales too
+    configs, (keys, ts, n, cfg, _) = random_config_trace(1000 + seed, 0 if seed >= 4 else 1 + seed % 3, 3000)
+    profile = seed % 2
+    c = oracle.OracleSim(profile)
+    p = P.Sim(profile)
+    for a, L, W in configs:
+        assert c.add_config(a, L, W) == p.add_config(a, L, W)
+    dec, rem, retry, reset, tok = c.decide(keys, ts, n, cfg)
+    for i in range(len(keys)):
+        d = p.decide(int(keys[i]), int(ts[i]), int(n[i]), int(cfg[i]), None)
         got = (int(dec[i]), int(rem[i]), int(retry[i]), int(reset[i]))
         assert got == d[:4], (i, got, d)
         if configs[cfg[i]][0] == 1 and d[0] in (0, 1):

@@ -53,6 +53,42 @@ def skewed_trace(seed, m, nkeys, configs, skews_ns=(0, -2_500_000_000, -7 * NS, 
     return keys, ts, n, cfg, sms
 
 
+def random_config_trace(seed, alg, m, nk=None):
+    """Seeded random configurations (limit 1 .. 1e12 log-uniform, window 1 ms
+    .. ~1 day) and a few hot keys whose gaps are drawn around each config's
+    refill period (limit / window): the chain's decades, multi-decade windows,
+    allows, clamps and expiries at scales the fixed configs above never reach;
+    for the window algorithms, runs that cross window starts at every scale."""
+    rng = np.random.default_rng(seed)
+    configs = []
+    for _ in range(3):
+        a = alg if alg else int(rng.integers(1, 4))
+        L = max(1, int(round(10 ** rng.uniform(0, 12))))
+        W = int(round(10 ** rng.uniform(6, 13.9)))
+        configs.append((a, L, W))
+    nk = nk or int(rng.integers(1, 5))
+    key = rng.integers(0, nk, m).astype(np.uint64)
+    cfg = (key % 3).astype(np.uint32)
+    period = np.array([W / L for _, L, W in configs])[cfg]          # ns per token
+    lim = np.array([L for _, L, _ in configs])[cfg]
+    # per phase of 3000 requests: a request takes a fraction f of the bucket and
+    # arrivals per refilled token drift around 1 -- long denial stretches (deep
+    # near-empty balances, decade crossings), refills to the cap, and allows
+    ph = m // 3000 + 1
+    f = np.repeat(10 ** rng.uniform(-6, -1, ph), 3000)[:m]
+    scale = np.repeat(10 ** rng.uniform(-1.5, 1, ph), 3000)[:m]
+    n = np.maximum(1, np.rint(lim * f)).astype(np.int64) * rng.choice([1, 1, 1, 2], m)
+    gaps = np.rint(rng.exponential(1.0, m) * period * n * scale / nk)
+    gaps[rng.random(m) < 0.05] = 0
+    gaps = np.minimum(gaps, 10 ** 12)                                # ts stays far from int64 overflow
+    r = rng.random(m)
+    big = r < 0.01
+    n[big] = np.maximum(1, (lim[big] * rng.random(int(big.sum())) * 1.3).astype(np.int64))
+    n[r > 0.999] = 1 << 62
+    ts = T0 + np.cumsum(gaps).astype(np.int64)
+    return configs, (key, ts, n, cfg, None)
+
+
 def q14_edge_values(n=4000, seed=5):
     """values just below / at / above powers of ten (where rounding to 14
     digits carries into the next decade, or must not), 14-digit midpoints,
