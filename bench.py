@@ -470,6 +470,10 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           # counts, then the chain's resolve cycles and counts the same way
                           "split_x16": [int(dbgw[70 + k]) * (16 if k in (0, 1, 4, 5) else 1) for k in range(8)]
                           + [int(dbgw[80]) * 16, int(dbgw[81]) * 16],
+                          # stamps builds: the chain round's pipeline model (two / three
+                          # summary buffers, sum of the rounds' max(producer, chain) work,
+                          # the chain's and the slowest producer's work over the rounds)
+                          "pipeline_model_x16": [int(dbgw[82 + k]) * 16 for k in range(5)],
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)

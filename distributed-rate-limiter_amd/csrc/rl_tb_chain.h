@@ -169,6 +169,9 @@ struct ChainShared {
     ChState st[2];
     ChSpec spec[2];                    // producers' speculative window of the round
     ChWin win[2];                      // the representation of tile[buf]'s window
+#ifdef RL_STAMPS
+    uint32_t wk[2];                    // the round's longest producer work (cycles / 16)
+#endif
 };
 
 __device__ inline double ring_add(const ChainShared& sh, uint32_t p) {
@@ -1680,7 +1683,19 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             reinterpret_cast<double*>(&sh.r_add[ring_slot(j0 >> 1)])[j0 & 1u] = add0;
         }
     }
+#ifdef RL_STAMPS
+    if (tid < 2) sh.wk[tid] = 0;
+    // pipeline model (chain wave, lane 0; cycles / 16): the finish times of the
+    // producers' and the chain's work per round with two summary buffers (the
+    // barrier schedule) and with three (producers one window further ahead)
+    // (a wave's round work is measured from the previous barrier's exit, so
+    // the round-top code every wave runs is in it)
+    uint64_t gP = 0, gC = 0, fP = 0, fC = 0, fC2 = 0, bsum = 0, csum = 0, psum = 0, tr0 = 0;
+#endif
     lds_barrier();
+#ifdef RL_STAMPS
+    CH_T(tr0);
+#endif
     const bool xd = CH_XDEC && profile == PROFILE_REDIS7;
     for (;;) {
         ChState s = sh.st[par];
@@ -1913,9 +1928,32 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         }
         par ^= 1u;
         CH_T(t0);
+#ifdef RL_STAMPS
+        const uint32_t wr = (uint32_t)((t0 - tr0) >> 4);
+        if (ch_producer_index(wave) >= 0 && lane == 0) atomicMax(&sh.wk[par], wr);
+#endif
         lds_barrier();
         CH_T(t1);
         cyc[3] += t1 - t0;
+#ifdef RL_STAMPS
+        tr0 = t1;
+        if (wave == 0 && lane == 0) {
+            // producers of round r summarize window r, the chain of round r
+            // resolves window r - 1; a buffer is free once its window is resolved
+            const uint64_t pr = sh.wk[par], cr = wr;
+            sh.wk[par] = 0;
+            const uint64_t nP2 = max(gP, gC) + pr, nC2 = max(gC, gP) + cr;
+            gP = nP2;
+            gC = nC2;
+            const uint64_t nP3 = max(fP, fC2) + pr, nC3 = max(fC, fP) + cr;
+            fC2 = fC;
+            fP = nP3;
+            fC = nC3;
+            bsum += max(pr, cr);
+            csum += cr;
+            psum += pr;
+        }
+#endif
     }
 #ifdef RL_STAMPS
     // dbg[24 + 4 * role + k]: role 0 chain (full / stop rounds, serial, barrier),
@@ -1927,8 +1965,17 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[24 + 4 * role + k], (uint32_t)(cyc[k] >> 4));
         if (role == 1)
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 2 ? cx[k] >> 4 : cx[k]));
-        if (role == 0)
+        if (role == 0) {
             for (int k = 4; k < 8; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 6 ? cx[k] >> 4 : cx[k]));
+            // dbg[82..86]: the pipeline model's two-buffer and three-buffer
+            // finish, the sum of the rounds' max(producer, chain) work, and the
+            // chain's and the slowest producer's work summed over the rounds
+            atomicAdd(&dbg[82], (uint32_t)max(gP, gC));
+            atomicAdd(&dbg[83], (uint32_t)max(fP, fC));
+            atomicAdd(&dbg[84], (uint32_t)bsum);
+            atomicAdd(&dbg[85], (uint32_t)csum);
+            atomicAdd(&dbg[86], (uint32_t)psum);
+        }
     }
 #endif
     if (tid == 0) {
