@@ -1690,7 +1690,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     // barrier schedule) and with three (producers one window further ahead)
     // (a wave's round work is measured from the previous barrier's exit, so
     // the round-top code every wave runs is in it)
-    uint64_t gP = 0, gC = 0, fP = 0, fC = 0, fC2 = 0, bsum = 0, csum = 0, psum = 0, tr0 = 0;
+    uint64_t gP = 0, gC = 0, fP = 0, fC = 0, fC2 = 0, bsum = 0, csum = 0, psum = 0, tr0 = 0, ttop = 0;
 #endif
     lds_barrier();
 #ifdef RL_STAMPS
@@ -1754,6 +1754,9 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         else if (s.mode != QM_NONE) P = rlq::pow10_exact(13 - s.E);
         nrounds++;
         CH_T(t0);
+#ifdef RL_STAMPS
+        ttop += t0 - tr0;   // the round top: from the barrier's exit to here
+#endif
         if (ch_producer_index(wave) >= 0) {
             const uint32_t pw = (uint32_t)ch_producer_index(wave);
             ChSpec sp{0u, 0u, 0u, 0u, 0, 0.0};
@@ -1975,6 +1978,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             atomicAdd(&dbg[84], (uint32_t)bsum);
             atomicAdd(&dbg[85], (uint32_t)csum);
             atomicAdd(&dbg[86], (uint32_t)psum);
+            atomicAdd(&dbg[87], (uint32_t)(ttop >> 4));   // the chain wave's round tops
         }
     }
 #endif
