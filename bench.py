@@ -10,13 +10,15 @@ table, radix sort by slot, segment discovery, per-key replay with exact Redis
 Lua "%.14g" semantics), inputs already resident in HBM, results written to HBM.
 
 Multi-GPU (one rank per GPU; `--gpus N` launches torch.distributed.run itself
-when WORLD_SIZE is unset): BASELINE configs[3] -- mixed per-tenant algorithms
-over 1B keys hash-sharded across the GPUs, every rank taking requests for any
-key, routed to the owner GPU and back by RCCL all-to-alls over xGMI
-(include/rl_route.h, shard.RoutedPipeline).  Per-GPU work is fixed ->
-"scaling": "weak".  The same JSON line carries secondary measurements: the
-metric's Zipf 1M-key workload routed over the same GPUs, and key-shard
-replicas (each rank its own keys, no data-path collective).
+when WORLD_SIZE is unset): the metric's own workload (configs[1], Zipf 1M
+keys) drawn by every rank from the whole key space and routed to the key's
+owner GPU and back by RCCL all-to-alls over xGMI (include/rl_route.h,
+shard.RoutedPipeline).  Per-GPU work is fixed -> "scaling": "weak".  The
+line carries `hot_owner_bound`: the hot key replays in order on its owner, so
+chain steps/s / hot share caps this workload on any N.  BASELINE configs[3]
+(mixed tenants over 1B keys) is reported beside it under its own metric name,
+routed and as key-shard replicas (each rank its own keys, no data-path
+collective), in `secondary`.
 
 Prints one JSON line (rank 0).
 """
@@ -242,6 +244,10 @@ KEYSPACE = {"tb_zipf": (1 << 21, 1024), "tb_zipf15": (1 << 21, 1024), "tb_hot": 
             "fw_uniform": (1024, 1 << 15), "sw_bursty": (1024, 1 << 27), "mixed": (1 << 26, 1 << 26)}
 
 
+class AgreedError(RuntimeError):
+    """an error every rank raises at the same point (agreed by an all_reduce)"""
+
+
 REPLAY_EVENT_STRIDE = 4   # replay timing events on every 4th launch of the timed region
 
 
@@ -273,6 +279,27 @@ def roofline_of(replay_ms, algs, uniq, m, workload):
             "launch_ms": per_launch_ms[dom]}, per_launch_ms
 
 
+def hot_chain_us(dbgw):
+    """the last batch's longest huge segment (the hot key's chain), start to
+    end in microseconds (replay kernel timeline words, 10 ns ticks)"""
+    return ((int(dbgw[17]) - int(dbgw[16])) & 0xffffffff) / 100.0
+
+
+def hot_owner_bound(hot_len, hot_us, m_total):
+    """The ceiling the hot key puts on the whole job: its requests replay in
+    order on one block of its owner GPU (tokenbucket.go:36-48 is a serial
+    recurrence), so no number of GPUs decides faster than chain rate / hot
+    share (12.4 % of every batch at Zipf 1.1)."""
+    if hot_len <= 0 or hot_us <= 0:
+        return None
+    rate = hot_len / (hot_us * 1e-6)
+    share = hot_len / m_total
+    return {"hot_key_requests_per_step": int(hot_len), "hot_share": share, "chain_us": hot_us,
+            "chain_steps_per_s": rate, "bound_decisions_per_s": rate / share,
+            "how": "the last step's hottest segment on its owner: chain steps/s (replay kernel timeline) / the "
+                   "key's share of all ranks' requests; no GPU count decides this workload faster"}
+
+
 def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     """each rank decides its own batches (N=1: the whole engine; N>1 with
     `sharded`: each rank owns a disjoint key space -- replicas)"""
@@ -287,7 +314,9 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     host = [gen.next_batch() for _ in range(nb + extra)]
     # sharded ingress: this rank's own key space (ids tagged with the rank)
     tag = np.uint64(rank if sharded else 0) << np.uint64(48)
-    uniq = np.unique(host[-1][0]).size
+    uniq, cnt = np.unique(host[-1][0], return_counts=True)
+    uniq, hot_len = uniq.size, int(cnt.max())
+    del cnt
     dev_batches = []
     for key, ts, n, cfg in host:
         dev_batches.append((
@@ -483,6 +512,8 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "light_batches": int(st.light_batches)},
         "latency": latency,
         "stamp_ring": stamp_ring,
+        "hot_owner_bound": hot_owner_bound(hot_len, hot_chain_us(dbgw), m) if workload.startswith("tb_zipf")
+        and not sharded else None,
         "stages_ms_per_batch": {k: v for k, v in zip(["probe", "sort", "segments", "replay", "finish"],
                                                     (stage_ms / max(nbat, 1)).tolist())},
         "stages_how": "HIP events on every stream, over the latency phase (after the timed region, which "
@@ -505,6 +536,9 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     nb = args.warmup + args.steps
     m = args.batch
     host = [gen.next_batch() for _ in range(nb)]
+    # the hot key (Zipf rank 1: every rank's generator shares the rank->id
+    # permutation) in this rank's last batch, for the hot-owner bound
+    hot_mine = int(np.count_nonzero(host[-1][0] == gen.keys.perm[0])) if hasattr(gen, "keys") else 0
     # bucket capacity per peer (every rank the same: the all-to-alls' equal
     # splits).  A uniform hash partition needs ~m / world plus a margin; a Zipf
     # hot key lands on one owner (12.4 % of every rank's batch at s = 1.1).
@@ -544,7 +578,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
                                 decide_ev=None if os.environ.get("RL_ROUTE_NO_EV") else eng.decide_routed_ev)
     outs = [(torch.empty(m, dtype=torch.uint8, device=dev),) +
             tuple(torch.empty(m, dtype=torch.int64, device=dev) for _ in range(3)) for _ in range(pipe.depth)]
-    def check(when):
+    def check(when):   # raises AgreedError on every rank alike
         # every rank takes the same branch (a rank that stopped alone would
         # leave the others in a collective): the worst code over the ranks
         rcs = [eng.sync(), router.sync(None)]
@@ -552,7 +586,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         for what, rc, mine in zip(("engine", "router"), t.tolist(), rcs):
             if rc != 0:
-                raise RuntimeError(f"{what} error during {when}: {rc}"
+                raise AgreedError(f"{what} error during {when}: {rc}"
                                    + (f" {eng.last_error()}" if mine else " (on another rank)")
                                    + (" (bucket overflow: raise RL_ROUTE_SLACK)" if rc == rl_amd.RL_EOVERFLOW else ""))
 
@@ -572,11 +606,18 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     check("timed region")
     stage_ms, nbat = eng.stage_times()
     st = eng.stats()
+    dbgw = eng.debug_words()
     eng.set_timing(0)
     tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     agg = [torch.zeros_like(tt) for _ in range(world)]
     dist.all_gather(agg, tt)
     elapsed = float(torch.stack(agg).max().cpu())
+    # the hot key's owner has the longest chain; its requests come from every rank
+    hot = torch.tensor([float(hot_mine), hot_chain_us(dbgw)], dtype=torch.float64, device=dev)
+    hot_sum = hot[:1].clone()
+    dist.all_reduce(hot_sum, op=dist.ReduceOp.SUM)
+    dist.all_reduce(hot, op=dist.ReduceOp.MAX)
+    hob = hot_owner_bound(int(hot_sum.item()), float(hot[1].item()), m * world) if hasattr(gen, "keys") else None
     # a hash partition: every owner receives ~m requests per step
     roof, _ = roofline_of(stage_ms[3] / nbat, algs, int(st.last_segments), m, workload)
     res = {
@@ -594,6 +635,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         if exchange else "none (world 1, buckets read in place)",
         "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3, "count_wait": pipe.wait_s / args.steps * 1e3},
         "roofline": roof,
+        "hot_owner_bound": hob,
     }
     del pipe, outs, ins
     eng.close()
@@ -613,8 +655,9 @@ def main():
                     help="timed steps (default: batches 5-60 of the 64-batch configs[1] trace)")
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1_000_000)
-    ap.add_argument("--workload", default=None, choices=sorted(WORKLOAD_DESC),
-                    help="default: tb_zipf (configs[1]) on 1 GPU, mixed (configs[3]) on N > 1")
+    ap.add_argument("--workload", default="tb_zipf", choices=sorted(WORKLOAD_DESC),
+                    help="default: tb_zipf (configs[1], the metric's Zipf 1M keys) on every N; on N > 1 "
+                         "configs[3] (mixed, 1B keys) is reported as a named secondary metric")
     ap.add_argument("--ingress", default=None, choices=["routed", "sharded"],
                     help="N > 1: routed (default; RCCL all-to-all to the key's owner) or sharded (replicas)")
     ap.add_argument("--no-secondary", action="store_true", help="N > 1: skip the secondary measurements")
@@ -659,7 +702,7 @@ def main():
     dev = torch.device("cuda", local_rank)
     pg_res = None
     ingress = args.ingress or ("routed" if world > 1 else "local")
-    workload = args.workload or ("mixed" if world > 1 else "tb_zipf")
+    workload = args.workload
     if world > 1 or ingress == "routed":
         # RCCL over xGMI: the request/count all-to-alls on the default group,
         # results on a second one (its own stream), barrier and timing
@@ -680,20 +723,27 @@ def main():
         res = bench_local(args, workload, world, rank, local_rank, dev, sharded=world > 1)
     secondary = []
     if world > 1 and not args.no_secondary:
-        # the metric's own workload over the same GPUs, and the replica mode
-        for wl, ing in (("tb_zipf", "routed"), (workload, "sharded")):
+        # configs[3] (the multi-GPU config: mixed tenants over 1B keys) routed
+        # and as key-shard replicas, each under its own metric name
+        for wl, ing in (("mixed", "routed"), ("mixed", "sharded")):
             if (wl, ing) == (workload, ingress):
                 continue
-            # a secondary line that fails is reported inside the line; the
-            # headline stands (the failure is the same on every rank: the
-            # routed checks agree over the ranks before raising)
             try:
                 r2 = (bench_routed(args, wl, world, rank, local_rank, dev, pg_res) if ing == "routed"
                       else bench_local(args, wl, world, rank, local_rank, dev, sharded=True))
-                secondary.append({k: r2[k] for k in ("value", "ms_per_step", "workload", "ingress")} |
-                                 {"unit": "decisions/s", "roofline_frac": r2["roofline"]["frac"]})
-            except (Exception, SystemExit) as ex:   # noqa: BLE001
+                secondary.append({"metric": f"decisions/sec @{world} GPU, configs[3] mixed tenants 1B keys "
+                                            f"({'routed to owners' if ing == 'routed' else 'key-shard replicas'})"}
+                                 | {k: r2[k] for k in ("value", "ms_per_step", "workload", "ingress")}
+                                 | {"unit": "decisions/s", "roofline_frac": r2["roofline"]["frac"]})
+            except AgreedError as ex:
+                # raised on every rank alike (the routed checks agree over the
+                # ranks first): report it inside the line, the headline stands
                 secondary.append({"workload": WORKLOAD_DESC.get(wl, wl), "ingress": ing, "error": str(ex)[:300]})
+            except BaseException as ex:   # noqa: BLE001
+                # raised on this rank alone: the other ranks may be waiting in a
+                # collective for it, so end the job instead of hanging it
+                print(f"rank {rank}: secondary {wl}/{ing} failed: {ex!r}", file=sys.stderr, flush=True)
+                os._exit(3)
     out = {
         "metric": "decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency",
         "value": res["value"],
@@ -718,7 +768,7 @@ def main():
     for k in ("unique_keys_per_batch", "batches_in_flight", "bucket_capacity", "host_ms_per_step", "collective_order"):
         if k in res:
             out["config"][k] = res[k]
-    for k in ("replay_detail", "latency", "stages_ms_per_batch", "stamp_ring"):
+    for k in ("hot_owner_bound", "replay_detail", "latency", "stages_ms_per_batch", "stamp_ring"):
         if res.get(k) is not None:
             out[k] = res[k]
     if secondary:

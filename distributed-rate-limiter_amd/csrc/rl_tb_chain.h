@@ -629,14 +629,17 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     // the tile prefix: in doubles when every lane's sum is below 2^46 (the
     // tile's then below 2^52: exact), else in int64
     double ex, inclD;
+    int64_t inclS;    // the exact tile sum (T.S: the nominal tile starts and runs' end states)
     if (__ballot(!(fabs(cum) < 0x1p46)) == 0ull) {
         inclD = wave_incl_scan_f64(cum);
         ex = inclD - cum;
+        inclS = (int64_t)inclD;
     } else {
         const int64_t Si = (int64_t)cum;
         const int64_t incl = wave_incl_scan_i64(Si);
         ex = (double)(incl - Si);
         inclD = (double)incl;
+        inclS = incl;
     }
     // the tile's bounds: lane 63 holds the reductions (no broadcast)
     const double ymin_t = wave_fold_f64(ymin - ex, __builtin_inf(), [](double x, double y) { return vmin_f64(x, y); });
@@ -663,7 +666,7 @@ __device__ __attribute__((always_inline)) inline void ch_produce(ChainShared& sh
     }
     if (lane == 63) {
         ChTile& T = sh.tile[buf][t];
-        T.S = (int64_t)inclD;
+        T.S = inclS;
         T.Sd = inclD;
         T.ymin = ymin_t;
         T.cmax = cmax_t;
@@ -1016,7 +1019,9 @@ __device__ __attribute__((always_inline)) inline ChOutcome ch_resolve(ChainShare
         if constexpr (MODE == QM_XDEC) {
             // the exact state stays within the producers' classification slack
             // of their estimate V, and below every allow / clamp threshold:
-            // |X - V| <= |X_t - V_t| + drift + the tile's offset changes
+            // |X - V| <= |X_t - V_t| + drift + the tile's offset changes,
+            // plus 4096 units for V's own rounding (valid below 2^60, which
+            // ch_produce_x enforces: rl_tb_xdec.h)
             const double bound = fabs(dD - T.cmax) + T.cmin + 2.0 * (double)moff + 4096.0;
             cand = forced || !(bound < T.dmax) || !(bound + 2.0 < T.ymin);
         } else {

@@ -409,12 +409,23 @@ __device__ __attribute__((always_inline)) inline void ch_produce_x(ChainShared& 
     int64_t r[K];
     int64_t Sr = 0;
     uint32_t nearm = 0, resm = 0;
-    double ymin = __builtin_inf(), slack = __builtin_inf(), dev = 0.0;
+    // The chain's commit test allows a fixed 4096 units for the rounding of
+    // V (rl_tb_chain.h ch_resolve_x).  That margin holds while every state
+    // estimate and vt PF stay below 2^60: the partial sums of A are then
+    // differences of two of them (< 2^61), every one of the 2K + 8 roundings
+    // on the way to a V is at most ulp(2^61) / 2 = 128 units (2560 in all),
+    // and the test's own conversions and subtractions add under 512.  A tile
+    // that reaches 2^60 anywhere gets slack -inf: it is never committed, the
+    // chain replays it exactly.
+    double ymin = __builtin_inf(), slack = fabs(Vl) < 0x1p60 && fabs(vt * PF) < 0x1p60 ? __builtin_inf()
+                                                                                        : -__builtin_inf();
+    double dev = 0.0;
 #pragma unroll
     for (int q = 0; q < K; q++) {
         const bool v = (uint32_t)q < nv;
         const double Vo = V + A[q];
         const double avi = fabs(V), avo = fabs(Vo);
+        slack = (v && !(avo < 0x1p60)) ? -__builtin_inf() : slack;
         const int kin = xk_of_d(avi), kout = xk_of_d(avo);
         const double g = xp10_d(kout);
         // the exact add * 10^(13 - E') (E' = F + kout: in units of the

@@ -21,6 +21,9 @@ order consistent with each rank's own order, under one monotone store clock.
 """
 from __future__ import annotations
 
+import collections
+import warnings
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -109,7 +112,7 @@ class RoutedPipeline:
     the buckets and results are read in place)."""
 
     def __init__(self, ops, decide, world, max_batch, device, pg_req=None, pg_res=None, depth=4, exchange=None,
-                 staged=False, lookahead=1, ordered=True, decide_ev=None):
+                 staged=False, lookahead=None, ordered=True, decide_ev=None):
         self.ops, self.decide, self.world = ops, decide, world
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
@@ -165,7 +168,14 @@ class RoutedPipeline:
                 s["ev_res"].record(self.R)    # materialize the event: the engine records it from now on
             self.slots.append(s)
         # result sides issued `lookahead` steps late (exchange only: without
-        # collectives there is nothing to order)
+        # collectives there is nothing to order).  Default 1, except on CUDA
+        # without decide_ev: there the decide call makes U wait for this
+        # step's engine at call time, so a late result side would queue step
+        # b-1's result collective behind engine(b) and serialize the steps
+        if lookahead is None:
+            lookahead = 0 if (self.cuda and self.decide_ev is None) else 1
+        elif lookahead > 0 and self.cuda and self.decide_ev is None and self.exchange:
+            warnings.warn("RoutedPipeline: lookahead > 0 without decide_ev serializes the engine's steps on CUDA")
         self.lookahead = max(0, int(lookahead)) if self.exchange else 0
         if depth <= self.lookahead:
             raise ValueError("depth must exceed lookahead (a buffer set is reused after its step unpacked)")
@@ -173,7 +183,8 @@ class RoutedPipeline:
         self._pend = []               # (b, slot, m, dec, rem, retry, reset): result side not issued yet
         self._ev_req = None           # after the last request-side collective issued (stream R)
         self._ev_res = None           # after the last result-side collective issued (stream U)
-        self.order_log = []           # ("req" | "res", step): the collective issue order (tests)
+        # ("req" | "res", step): the collective issue order, the last 4096 (tests)
+        self.order_log = collections.deque(maxlen=4096)
         self.collectives = 0          # all-to-alls issued (tests: the exchange really ran)
         self.wait_s = 0.0             # host time spent waiting on the device: none by construction
         self.host_prof = {}

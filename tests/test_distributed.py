@@ -89,7 +89,7 @@ def _pipeline_worker(rank, world, port, q, m=3000, cap=4096, exchange=None):
         # result exchange between step b + 1's and b + 2's request exchanges
         nb = len(mine)
         want = [("req", 0)] + [x for b in range(1, nb) for x in (("req", b), ("res", b - 1))] + [("res", nb - 1)]
-        ok = ok and pipe.order_log == want
+        ok = ok and list(pipe.order_log) == want
         q.put((rank, ok, ops.overflow))
     finally:
         dist.destroy_process_group()

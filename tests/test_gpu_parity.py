@@ -9,7 +9,7 @@ import pytest
 
 import oracle
 import traces
-from tracegen import CONFIG_SETS, T0, NS, random_config_trace, random_trace, skewed_trace
+from tracegen import CONFIG_SETS, T0, NS, long_window_trace, random_config_trace, random_trace, skewed_trace
 
 pytestmark = pytest.mark.gpu
 
@@ -178,6 +178,21 @@ def test_chain_random_configs(rl, seed):
 def test_window_random_configs(rl, seed):
     configs, tr = random_config_trace(800 + seed, 2 + seed % 2 if seed < 4 else 0, 90_000)
     run_both(rl, seed % 2, configs, split(tr, [30_000, 60_000]), tb=1 << 12, win=1 << 12)
+
+
+@pytest.mark.parametrize("wi", range(3))
+@pytest.mark.parametrize("alg", [1, 2, 3, 0])
+@pytest.mark.parametrize("profile", [0, 1])
+def test_long_windows(rl, profile, alg, wi):
+    """Windows of 1 to 365 days (config.go:41-46 accepts up to 365 d): 7-day
+    windows (year-1 Truncate offset, fixedwindow.go:72), W = 2^24 s + 1 ns and
+    31535999.999999999 s (Duration.Seconds() rounds up into ttl, pws and rate:
+    tokenbucket.go:155-157,170, slidingwindow.go:74-75,161-162,
+    fixedwindow.go:151), W = 365 d with L = 1 (refill 3.2e-8 tokens/s), limits
+    up to 1e12.  A hot key per config through the chain (huge segments in the
+    second batch) and the wave replay, 20k light keys, time spanning years."""
+    configs, tr = long_window_trace(1100 + 10 * wi + alg + 5 * profile, alg, 120_000, wi=wi)
+    run_both(rl, profile, configs, split(tr, [3000, 27_000, 90_000]), tb=1 << 16, win=1 << 16)
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -373,21 +388,28 @@ def test_config3_mixed(rl):
     run_both(rl, 0, g.configs, [g.next_batch() for _ in range(2)], tb=1 << 19, win=1 << 20)
 
 
-def test_config3_per_gpu_scale(rl):
-    """BASELINE configs[3] at its per-GPU share: 1B keys hash-sharded over 8
-    GPUs is 125M keys per GPU.  Mixed tenants (cfg = key mod 3: TB 20/12s, SW
-    100/60s, FW 100/60s), 132M requests in 2M batches over ~132 s of virtual
-    time, tables sized for the share (TB 2^26, window 2^27 + spill 2^28: 18 GB
-    of HBM).  As configs[2]: a seeded 1/32 of the keys replayed by the oracle
-    bit for bit, and whole-run properties -- every request decided, the entries
-    used equal the distinct keys of each table, live spilled window keys."""
-    g = traces.MixedTenants(nkeys=125_000_000, batch=2_000_000)
-    eng = make_engine(rl, 0, tb=1 << 26, win=1 << 27, max_batch=1 << 21)
+@pytest.mark.parametrize("gpus", [8, 2])
+def test_config3_per_gpu_scale(rl, gpus):
+    """BASELINE configs[3] at its per-GPU share: 1B keys hash-sharded over G
+    GPUs is 125M keys per GPU at G = 8 and 500M at G = 2.  Mixed tenants
+    (cfg = key mod 3: TB 20/12s, SW 100/60s, FW 100/60s) in 2M batches at
+    1 us mean gaps, tables sized for the share at load ~0.6 (G = 8: TB 2^26,
+    window 2^27 + spill 2^28, 18 GB of HBM; G = 2: TB 2^28, window 2^29 +
+    spill 2^30, 72 GB).  G = 8 runs 132M requests (~80M distinct keys), G = 2
+    256M (~200M distinct keys).  As configs[2]: a seeded 1/32 of the keys
+    replayed by the oracle bit for bit, and whole-run properties -- every
+    request decided, the entries used equal the distinct keys of each table,
+    live spilled window keys."""
+    share = 1_000_000_000 // gpus
+    sh = 26 if gpus == 8 else 28
+    nb = 66 if gpus == 8 else 128
+    g = traces.MixedTenants(nkeys=share, batch=2_000_000)
+    eng = make_engine(rl, 0, tb=1 << sh, win=1 << (sh + 1), max_batch=1 << 21)
     sim = oracle.OracleSim(0)
     for c in g.configs:
         assert eng.register(*c) == sim.add_config(*c)
-    seen = []
-    for b in range(66):
+    seen = np.zeros(share, np.bool_)
+    for b in range(nb):
         key, ts, n, cfg = g.next_batch()
         res = eng.decide(key, ts, n, cfg, want_tokens=(b % 8 == 0))
         assert np.all(res.decision <= 1), f"batch {b}"
@@ -396,13 +418,13 @@ def test_config3_per_gpu_scale(rl):
         sub = rl.Decisions(res.decision[pick], res.remaining[pick], res.retry_after_ns[pick],
                            res.reset_at_ns[pick], None if res.tokens is None else res.tokens[pick])
         assert_same(sub, ref, g.configs, cfg[pick], what=f"batch {b}")
-        seen.append(np.unique(key))
-    allk = np.unique(np.concatenate(seen))
+        seen[key] = True
+    distinct = int(np.count_nonzero(seen))
+    tb_keys = int(np.count_nonzero(seen[0::3]))
     del seen
-    tb_keys = int(np.count_nonzero(allk % np.uint64(3) == np.uint64(0)))
     info = eng.table_info(int(ts[-1]) // 1_000_000)
-    assert allk.size > 80_000_000
-    assert info.tb_used == tb_keys and info.win_used == allk.size - tb_keys
+    assert distinct > (80_000_000 if gpus == 8 else 190_000_000)
+    assert info.tb_used == tb_keys and info.win_used == distinct - tb_keys
     assert info.spill_used > 0 and info.spill_live > 0
     assert eng.sync() == 0
     eng.close()

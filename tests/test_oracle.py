@@ -134,6 +134,27 @@ def test_c_vs_python_random_configs(lib, seed):
             assert tok[i] == d[4] or (math.isnan(tok[i]) and math.isnan(d[4]))
 
 
+@pytest.mark.parametrize("wi", range(3))
+@pytest.mark.parametrize("alg", [1, 2, 3, 0])
+def test_c_vs_python_long_windows(lib, alg, wi):
+    # the GPU suite's long windows (1 d .. 365 d, Seconds() rounding at 2^24 s,
+    # refill rates down to 3e-8 tokens/s): both restatements agree there too
+    from tracegen import long_window_trace
+    configs, (keys, ts, n, cfg, _) = long_window_trace(1200 + 10 * wi + alg, alg, 4000, wi=wi, n_light=300)
+    profile = (alg + wi) % 2
+    c = oracle.OracleSim(profile)
+    p = P.Sim(profile)
+    for a, L, W in configs:
+        assert c.add_config(a, L, W) == p.add_config(a, L, W)
+    dec, rem, retry, reset, tok = c.decide(keys, ts, n, cfg)
+    for i in range(len(keys)):
+        d = p.decide(int(keys[i]), int(ts[i]), int(n[i]), int(cfg[i]), None)
+        got = (int(dec[i]), int(rem[i]), int(retry[i]), int(reset[i]))
+        assert got == d[:4], (i, got, d)
+        if configs[cfg[i]][0] == 1 and d[0] in (0, 1):
+            assert tok[i] == d[4] or (math.isnan(tok[i]) and math.isnan(d[4]))
+
+
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("kind", ["sw", "fw", "mixed"])
 def test_c_vs_python_skewed_clocks(lib, profile, kind):

@@ -89,6 +89,62 @@ def random_config_trace(seed, alg, m, nk=None):
     return configs, (key, ts, n, cfg, None)
 
 
+DAY = 86400 * NS
+# windows Validate accepts past a day (config.go:41-46: 1 ms <= W <= 365 d):
+# one day; seven days (Truncate's year-1 offset is 259200 s, fixedwindow.go:72);
+# 2^24 s and 31535999.999999999 s, where Duration.Seconds() rounds up
+# (31536000.0: ttl, pws and rate all shift, tokenbucket.go:155-157,170,
+# fixedwindow.go:151, slidingwindow.go:75,161-162); 365 days exactly; 30 days
+LONG_WINDOWS = [DAY, 7 * DAY, 31_535_999_999_999_999, 365 * DAY, (1 << 24) * NS + 1, 30 * DAY]
+
+
+def long_window_trace(seed, alg, m, wi=0, n_light=20_000, hot_share=0.6):
+    """Reference-legal long windows (1 day .. 365 days) with limits 1 .. 1e12,
+    so refill rates reach ~3e-8 tokens/s (L = 1, W = 365 d).  Three configs
+    (key id mod 3): LONG_WINDOWS[wi] and LONG_WINDOWS[wi + 3], then a random
+    window in [1 d, 365 d]; the first config's limit is 1 when wi is even,
+    the third's is in [1e9, 1e12].  One hot key per config carries
+    hot_share / 3 of the traffic (chain and wave segments) among n_light light
+    keys.  Time runs in phases of 3000 requests at a gap scale around each hot
+    key's refill period (capped at 1000 s), with jumps of hours to ~400 days
+    between phases, so window starts of every config are crossed and buckets
+    go from deep denial to the cap; the whole trace spans a few years."""
+    rng = np.random.default_rng(seed)
+    configs = []
+    for i in range(3):
+        a = alg if alg else int(rng.integers(1, 4))
+        if i < 2:
+            W = LONG_WINDOWS[(wi + 3 * i) % len(LONG_WINDOWS)]
+        else:
+            W = int(round(10 ** rng.uniform(np.log10(DAY), np.log10(365 * DAY))))
+        if i == 0 and wi % 2 == 0:
+            L = 1
+        else:
+            L = max(1, int(round(10 ** rng.uniform(9 if i == 2 else 0, 12))))
+        configs.append((a, L, W))
+    hot = rng.random(m) < hot_share
+    key = np.where(hot, rng.integers(0, 3, m), rng.integers(3, 3 + n_light, m)).astype(np.uint64)
+    cfg = (key % 3).astype(np.uint32)
+    period = np.array([W / L for _, L, W in configs])[cfg]          # ns per token
+    lim = np.array([L for _, L, _ in configs])[cfg]
+    ph = m // 3000 + 1
+    f = np.repeat(10 ** rng.uniform(-6, -0.5, ph), 3000)[:m]
+    scale = np.repeat(10 ** rng.uniform(-2, 1, ph), 3000)[:m]
+    n = np.maximum(1, np.rint(lim * f)).astype(np.int64) * rng.choice([1, 1, 1, 2], m)
+    gaps = np.rint(rng.exponential(1.0, m) * np.minimum(period * n * scale * hot_share / 3, 1e12))
+    gaps[rng.random(m) < 0.05] = 0
+    jumps = rng.choice([0, 3600 * NS, DAY, 5 * DAY, 40 * DAY, 400 * DAY], ph, p=[0.3, 0.2, 0.2, 0.15, 0.1, 0.05])
+    jumps = (jumps * rng.random(ph)).astype(np.int64)
+    gaps[::3000] += jumps[: gaps[::3000].size]
+    r = rng.random(m)
+    big = r < 0.01
+    n[big] = np.maximum(1, (lim[big] * rng.random(int(big.sum())) * 1.3).astype(np.int64))
+    n[r > 0.999] = 1 << 62
+    ts = T0 + np.cumsum(gaps).astype(np.int64)
+    assert int(ts[-1]) - T0 < 40 * 365 * DAY
+    return configs, (key, ts, n, cfg, None)
+
+
 def q14_edge_values(n=4000, seed=5):
     """values just below / at / above powers of ten (where rounding to 14
     digits carries into the next decade, or must not), 14-digit midpoints,
