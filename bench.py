@@ -312,6 +312,25 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     lat_n = max(0, args.lat_batches) if world == 1 else 0
     extra = lat_n if lat_n else 4      # batches after the timed region (latency / stage breakdown)
     host = [gen.next_batch() for _ in range(nb + extra)]
+    if os.environ.get("RL_BENCH_HOME_SORT"):
+        # A/B experiment only: each batch stably reordered by the key's home
+        # slot in the engine's tables ("full") or by its top 8 bits ("digit"),
+        # to price a probe that walks the table in home order (per-key order
+        # is kept, so decisions are those of a valid trace)
+        import shard
+        tb_cap, win_cap = KEYSPACE[workload]
+        bits = int(tb_cap + win_cap).bit_length()
+        tbc = np.array([a == 1 for a, _, _ in gen.configs])
+        out = []
+        for key, ts, n, cfg in host:
+            h = shard.mix64(key)
+            is_tb = tbc[cfg]
+            g = np.where(is_tb, h & np.uint64(tb_cap - 1), np.uint64(tb_cap) + (h & np.uint64(win_cap - 1)))
+            if os.environ["RL_BENCH_HOME_SORT"] == "digit":
+                g = g >> np.uint64(bits - 8)
+            o = np.argsort(g, kind="stable")
+            out.append((key[o], ts[o], n[o], cfg[o]))
+        host = out
     # sharded ingress: this rank's own key space (ids tagged with the rank)
     tag = np.uint64(rank if sharded else 0) << np.uint64(48)
     uniq, cnt = np.unique(host[-1][0], return_counts=True)
@@ -745,7 +764,10 @@ def main():
                 print(f"rank {rank}: secondary {wl}/{ing} failed: {ex!r}", file=sys.stderr, flush=True)
                 os._exit(3)
     out = {
-        "metric": "decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency",
+        # BASELINE.json's metric names the Zipf 1M-key workload; a run of
+        # another workload (--workload) is named by it instead
+        "metric": ("decisions/sec @1/8 GPU, Zipf 1M keys; % HBM roofline; p99 batch latency"
+                   if workload == "tb_zipf" else f"decisions/sec @{world} GPU, {WORKLOAD_DESC[workload]}"),
         "value": res["value"],
         "unit": "decisions/s",
         "n_gpus": world,

@@ -2127,7 +2127,11 @@ __device__ __attribute__((always_inline)) inline void replay_rest(const uint32_t
             const SegRec sg = L.list[1][u];
             const uint32_t k0 = sk[sg.j0];
             // a key the batch inserted, alone in it: the absent state, unread
+#ifdef RL_AB_ALLFRESH   // timing experiment only (wrong results): no table read in the light phase
+            const bool fresh = sg.len == 1u;
+#else
             const bool fresh = sg.len == 1u && a.fresh && a.fresh[sg.j0];
+#endif
             if (k0 < win_base) replay_tb_serial(&tb[k0], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, fresh);
             else replay_win_serial(&win[k0 - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a, eflags, fresh);
         }
