@@ -244,6 +244,10 @@ KEYSPACE = {"tb_zipf": (1 << 21, 1024), "tb_zipf15": (1 << 21, 1024), "tb_hot": 
             "fw_uniform": (1024, 1 << 15), "sw_bursty": (1024, 1 << 27), "mixed": (1 << 26, 1 << 26)}
 
 
+REHEARSE = [False]     # --rehearse-gloo (main)
+CDEV = [None]          # device of the small collective tensors: the GPU (RCCL), the CPU (gloo)
+
+
 class AgreedError(RuntimeError):
     """an error every rank raises at the same point (agreed by an all_reduce)"""
 
@@ -361,7 +365,7 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     algs = {a for a, _, _ in gen.configs}
     tb_cap, win_cap = KEYSPACE[workload]
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=tb_cap, win_capacity=win_cap,
-                        max_batch=args.batch, device=local_rank,
+                        max_batch=args.batch, device=dev.index,
                         # inputs are resident before the timed region: batch b+1's
                         # hash/sort/permute overlaps batch b's replay
                         flags=0 if args.no_pipeline else rl_amd.OPT_PIPELINE)
@@ -471,7 +475,7 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     stage_ms, nbat = eng.stage_times()
     eng.set_timing(0)
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=CDEV[0])
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     roof, per_launch_ms = roofline_of(replay_ms, algs, uniq, m, workload)
@@ -571,7 +575,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         cap = min(m, int(np.ceil(slack * m / world)))
     else:
         need = max(int(np.bincount(shard.owner_of(k, world), minlength=world).max()) for k, _, _, _ in host)
-        need_t = torch.tensor([need], dtype=torch.int64, device=dev)
+        need_t = torch.tensor([need], dtype=torch.int64, device=CDEV[0])
         dist.all_reduce(need_t, op=dist.ReduceOp.MAX)
         cap = min(m, max(int(need_t.item()), int(np.ceil(1.05 * m / world))))
     ins = [(torch.from_numpy(k.view(np.int64)).to(dev), torch.from_numpy(t).to(dev), torch.from_numpy(n).to(dev),
@@ -579,9 +583,9 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     del host
     algs = {a for a, _, _ in gen.configs}
     tb_cap, win_cap = KEYSPACE[workload]
-    router = rl_amd.Router(local_rank, world, m, cap)
+    router = rl_amd.Router(dev.index, world, m, cap)
     eng = rl_amd.Engine(profile=rl_amd.PROFILE_REDIS7, tb_capacity=tb_cap, win_capacity=win_cap,
-                        max_batch=world * router.capacity, device=local_rank, flags=0)
+                        max_batch=world * router.capacity, device=dev.index, flags=0)
     for a, L, W in gen.configs:
         eng.register(a, L, W)
     exchange = world > 1 or args.route_exchange
@@ -589,7 +593,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     # RL_ROUTE_ONE_PG=1 (both directions on the default group: one stream
     # orders them), RL_ROUTE_UNORDERED=1 (no cross-group waits)
     one_pg = bool(os.environ.get("RL_ROUTE_ONE_PG"))
-    pipe = shard.RoutedPipeline(router, eng.decide_routed, world, m, dev, pg_req=None,
+    pipe = shard.RoutedPipeline(router, eng.decide_routed, world, m, dev, pg_req=None, staged=REHEARSE[0],
                                 pg_res=None if one_pg else pg_res,
                                 depth=int(os.environ.get("RL_ROUTE_DEPTH", "4")), exchange=exchange,
                                 lookahead=int(os.environ.get("RL_ROUTE_LOOKAHEAD", "1")),
@@ -601,7 +605,7 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         # every rank takes the same branch (a rank that stopped alone would
         # leave the others in a collective): the worst code over the ranks
         rcs = [eng.sync(), router.sync(None)]
-        t = torch.tensor(rcs, dtype=torch.int64, device=dev)
+        t = torch.tensor(rcs, dtype=torch.int64, device=CDEV[0])
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         for what, rc, mine in zip(("engine", "router"), t.tolist(), rcs):
             if rc != 0:
@@ -627,12 +631,12 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
     st = eng.stats()
     dbgw = eng.debug_words()
     eng.set_timing(0)
-    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=CDEV[0])
     agg = [torch.zeros_like(tt) for _ in range(world)]
     dist.all_gather(agg, tt)
     elapsed = float(torch.stack(agg).max().cpu())
     # the hot key's owner has the longest chain; its requests come from every rank
-    hot = torch.tensor([float(hot_mine), hot_chain_us(dbgw)], dtype=torch.float64, device=dev)
+    hot = torch.tensor([float(hot_mine), hot_chain_us(dbgw)], dtype=torch.float64, device=CDEV[0])
     hot_sum = hot[:1].clone()
     dist.all_reduce(hot_sum, op=dist.ReduceOp.SUM)
     dist.all_reduce(hot, op=dist.ReduceOp.MAX)
@@ -645,7 +649,8 @@ def bench_routed(args, workload, world, rank, local_rank, dev, pg_res):
         "workload": WORKLOAD_DESC[workload],
         "ingress": (f"routed: owner = hash(key) mod {world}; per peer a fixed-capacity bucket of "
                     f"{router.capacity} 32-B request records and one of 32-B results, moved by equal-split "
-                    f"RCCL all-to-alls over xGMI" + ("" if exchange else " (world 1: buckets read in place)")
+                    + ("gloo all-to-alls through host memory (--rehearse-gloo: ranks share one GPU)" if REHEARSE[0]
+                       else "RCCL all-to-alls over xGMI") + ("" if exchange else " (world 1: buckets read in place)")
                     + "; merge and engine sized on the device, no host read in the step (include/rl_route.h)"),
         "batch": m,
         "bucket_capacity": router.capacity,
@@ -684,6 +689,9 @@ def main():
                     help="--ingress routed at N = 1: run the loopback all-to-alls too (the N > 1 step's work)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="cpu_baseline requests per host core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="N > 1 rehearsal on a one-GPU box: every rank on GPU 0, collectives over gloo (not a "
+                         "measurement)")
     ap.add_argument("--no-pipeline", action="store_true", help="one batch in flight at a time")
     ap.add_argument("--lat-batches", type=int, default=32,
                     help="batches of the latency phase (after the timed region): closed loop with the "
@@ -717,8 +725,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # --rehearse-gloo: every rank on GPU 0, collectives over gloo through host
+    # memory -- the N > 1 code path of this script on a one-GPU box (the
+    # numbers are not a measurement: ranks share one GPU)
+    REHEARSE[0] = args.rehearse_gloo
+    gpu = 0 if args.rehearse_gloo else local_rank
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    CDEV[0] = torch.device("cpu") if args.rehearse_gloo else dev
     pg_res = None
     ingress = args.ingress or ("routed" if world > 1 else "local")
     workload = args.workload
@@ -734,8 +748,12 @@ def main():
         if not os.environ.get("RL_ROUTE_PG_NORMAL"):
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = True
-        dist.init_process_group("nccl", device_id=dev, pg_options=opts)
-        pg_res = dist.new_group(backend="nccl")
+        if args.rehearse_gloo:
+            dist.init_process_group("gloo")
+            pg_res = dist.new_group(backend="gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev, pg_options=opts)
+            pg_res = dist.new_group(backend="nccl")
     if ingress == "routed":
         res = bench_routed(args, workload, world, rank, local_rank, dev, pg_res)
     else:
