@@ -419,6 +419,7 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
     t0 = time.perf_counter()
     for b in range(args.warmup, nb):
         step(b)
+    t_host = time.perf_counter() - t0   # the host's enqueue time (device work runs behind it)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -496,6 +497,7 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
         else "local",
         "batch": m, "unique_keys_per_batch": uniq,
         "batches_in_flight": 1 if args.no_pipeline else 3,
+        "host_ms_per_step": {"enqueue": t_host / args.steps * 1e3},
         "roofline": roof,
         "replay_detail": {"heavy_segments": int(st.last_heavy), "segments": int(st.last_segments),
                           "stamp_cycles_longest_segment": [int(x) for x in st.stamp_cycles],

@@ -169,6 +169,8 @@ struct ChainShared {
     ChState st[2];
     ChSpec spec[2];                    // producers' speculative window of the round
     ChWin win[2];                      // the representation of tile[buf]'s window
+    double plan_s[CH_NP], plan_sp[CH_NP];   // ch_plan_par: each producer wave's tile sums
+    uint32_t plan_tag[CH_NP];               // and the plan number they belong to (0 at kernel start)
 #ifdef RL_STAMPS
     uint32_t wk[2];                    // the round's longest producer work (cycles / 16)
 #endif
@@ -1632,9 +1634,14 @@ struct XPlanW {
     double vt;        // the calling producer's tile start estimate
 };
 __device__ XDEC_FN XPlanW ch_plan_w(ChainLds* shp, uint32_t first, uint32_t cnt, double v0,
-                                                    uint32_t pw) {
-    const ChainShared& sh = *(const ChainShared*)shp;
+                                                    uint32_t pw, uint32_t seq) {
+    ChainShared& sh = *(ChainShared*)shp;
+#ifdef RL_PLAN_SEQ   // A/B: every producer wave sums the whole window
+    (void)seq;
     const XPlan pl = ch_plan(sh, first, cnt, v0);
+#else
+    const XPlan pl = ch_plan_par(sh, first, cnt, v0, pw, seq);
+#endif
     return XPlanW{pl.mode, pl.E, pick(pl.vt, pw)};
 }
 __device__ XDEC_FN void ch_produce_xw(ChainLds* shp, uint32_t buf, uint32_t t, uint32_t pfirst,
@@ -1649,7 +1656,7 @@ template <bool LCFG>
 __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh, TbEntry* e, uint32_t j0, uint32_t j1,
                                                                 const CfgDev* __restrict__ cfgs, int32_t profile,
                                                                 const ReqArgs& a, const TbPre& pre, uint32_t* eflags,
-                                                                uint32_t* dbg, const TbRuns& runs) {
+                                                                uint32_t* dbg, const TbRuns& runs, uint32_t& plan_seq) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t nrounds = 0, iters = 0, par = 0, nserial = 0;
     uint64_t cyc[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0;
@@ -1781,7 +1788,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             double dmax = (double)DEC_HI;
             if (sp.valid) {
                 if (xd) {
-                    pl = ch_plan_w(shl, sp.first, sp.cnt, sp.v0, pw);
+                    pl = ch_plan_w(shl, sp.first, sp.cnt, sp.v0, pw, ++plan_seq);
                     if (pl.mode == QM_NONE) sp.valid = 0u;
                 } else {
                     pl.mode = QM_DEC;
@@ -1822,7 +1829,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
 #pragma unroll
                         for (int t = 0; t < CH_NP; t++) Xe += (uint32_t)t < nt ? sh.tile[s.cbuf][t].S : 0;
                     }
-                    pl = ch_plan_w(shl, wf, wc, st_value(Xe, s.E, s.mode), pw);
+                    pl = ch_plan_w(shl, wf, wc, st_value(Xe, s.E, s.mode), pw, ++plan_seq);
                 }
             }
             if (pw == 0 && (threadIdx.x & 63) == 0) {
@@ -2174,6 +2181,8 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
     const uint32_t nhuge = L.count[3];
     if (blockIdx.x == 0 && threadIdx.x == 0 && h_huge) *(volatile uint32_t*)h_huge = nhuge;
     if (!replay_joins(L, grid_base, light_min)) return;
+    if (threadIdx.x < (uint32_t)CH_NP) sh.plan_tag[threadIdx.x] = 0u;   // (the claim loop's barrier follows)
+    uint32_t plan_seq = 0;   // ch_plan_par numbers (the same in every producer wave)
     // timeline (10 ns ticks, low 32 bits): dbg[13] = ~first block start,
     // dbg[14] = last block end, dbg[16/17] = longest segment start / end
     if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
@@ -2219,7 +2228,8 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
         if (u == NO_STOP) break;
         const SegRec sg = L.list[3][u];
         const uint64_t t_seg = __builtin_amdgcn_s_memrealtime();
-        ch_segment<LCFG>(sh, &tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs);
+        ch_segment<LCFG>(sh, &tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, dbg, runs,
+                         plan_seq);
         __syncthreads();
         if (threadIdx.x == 0 && dbg) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();

@@ -364,6 +364,79 @@ __device__ __attribute__((always_inline)) inline XPlan ch_plan(const ChainShared
     return pl;
 }
 
+// The same plan with the window's tiles split over the producer waves: wave
+// pw sums tile pw alone (one ring read, two reductions instead of six and
+// twelve), publishes its sums in LDS under the round's plan number `seq`, and
+// every wave combines the six tiles in tile order -- the same operations on
+// the same values as ch_plan, so the same plan.  All producer waves make the
+// same sequence of plan calls (the plan's condition is block-uniform), so
+// their seq counters agree.  A wave whose wait passes a bound (never
+// expected) computes the whole plan itself.
+__device__ __attribute__((always_inline)) inline XPlan ch_plan_par(ChainShared& sh, uint32_t first, uint32_t cnt,
+                                                                  double v0, uint32_t pw, uint32_t seq) {
+    constexpr int K = CH_K;
+    const uint32_t lane = threadIdx.x & 63;
+    {
+        double s = 0.0, sp = 0.0;
+        double ra[K], rt[K];
+        ring_read_k(sh, first + pw * CH_TILE + lane * K, ra, rt);
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            const uint32_t o = pw * CH_TILE + lane * K + q;
+            const double ad = ra[q];
+            const double x = (o < cnt && fabs(ad) < 1e300) ? ad : 0.0;
+            s += x;
+            sp += x > 0.0 ? x : 0.0;
+        }
+        const double S = wave_reduce_f64(s, 0.0, [](double x, double y) { return x + y; });
+        const double Sp = wave_reduce_f64(sp, 0.0, [](double x, double y) { return x + y; });
+        if (lane == 0) {
+            sh.plan_s[pw] = S;
+            sh.plan_sp[pw] = Sp;
+            __hip_atomic_store(&sh.plan_tag[pw], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    bool ok = true;
+#pragma unroll
+    for (int t = 0; t < CH_NP; t++) {
+        uint32_t spins = 0;
+        while (__hip_atomic_load(&sh.plan_tag[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != seq) {
+            if (++spins > (1u << 20)) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (!ok) return ch_plan(sh, first, cnt, v0);
+    XPlan pl;
+    double v = v0, lo = v0, hi = v0;
+#pragma unroll
+    for (int t = 0; t < CH_NP; t++) {
+        pl.vt[t] = v;
+        const double S = sh.plan_s[t], Sp = sh.plan_sp[t];
+        hi = fmax(hi, v + Sp);
+        lo = fmin(lo, v - (Sp - S));
+        v += S;
+    }
+    pl.mode = QM_NONE;
+    pl.E = 0;
+    if (!(lo == lo) || !(hi == hi) || !(fabs(lo) < 1e12) || !(fabs(hi) < 1e12)) return pl;
+    if (lo > 0.0) {
+        const int E = (int)floor(log10(lo));
+        if (E >= -9 && E <= 12 && lo > rlq::pow10_exact(E + 9) * 1e-9 * (1.0 + 1e-12) &&
+            hi < rlq::pow10_exact(E + 10) * 1e-9 * (1.0 - 1e-12)) {
+            pl.mode = QM_DEC;
+            pl.E = E;
+            return pl;
+        }
+    }
+    const double m = fmax(fabs(lo), fabs(hi));
+    const int Et = m > 0.0 ? (int)floor(log10(m)) : XDEC_FMIN + 4;
+    const int F = max(Et - 4, XDEC_FMIN);
+    if (F > XDEC_FMAX) return pl;
+    pl.mode = QM_XDEC;
+    pl.E = F;
+    return pl;
+}
+
 // ulp of a positive normal double
 __device__ inline double ulp_pos(double z) {
     const int64_t e = (__double_as_longlong(z) >> 52) & 0x7ff;
