@@ -1665,6 +1665,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     // of one-decade / multi-decade windows and their counts, chain resolve
     // cycles of one-decade / multi-decade windows and their counts
     uint64_t cx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t cplan = 0;   // producer 0: plan cycles (dbg[88])
 #endif
     (void)t0; (void)t1;
     TbLoader L;
@@ -1832,6 +1833,11 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
                     pl = ch_plan_w(shl, wf, wc, st_value(Xe, s.E, s.mode), pw, ++plan_seq);
                 }
             }
+#ifdef RL_STAMPS
+            uint64_t tpl;
+            CH_T(tpl);
+            cplan += tpl - t1;   // the plan (one-decade bound or multi-decade plan)
+#endif
             if (pw == 0 && (threadIdx.x & 63) == 0) {
                 sp.buf = s.pbuf;
                 sh.spec[par ^ 1u] = sp;
@@ -1978,8 +1984,10 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         const uint32_t role = wave == 0 ? 0u : wave == 1 ? 1u : wave == (uint32_t)CH_LOADER ? 2u : 3u;
         if (role < 3)
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[24 + 4 * role + k], (uint32_t)(cyc[k] >> 4));
-        if (role == 1)
+        if (role == 1) {
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 2 ? cx[k] >> 4 : cx[k]));
+            atomicAdd(&dbg[88], (uint32_t)(cplan >> 4));
+        }
         if (role == 0) {
             for (int k = 4; k < 8; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 6 ? cx[k] >> 4 : cx[k]));
             // dbg[82..86]: the pipeline model's two-buffer and three-buffer
