@@ -530,7 +530,7 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "pipeline_model_x16": [int(dbgw[82 + k]) * 16 for k in range(5)],
                           "chain_round_tops_x16": int(dbgw[87]) * 16,
                           # stamps build: producer 0's plan cycles (after the exit guess)
-                          "producer_plan_x16": int(dbgw[88]) * 16,
+                          "producer_plan_x16": int(dbgw[48]) * 16,
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)

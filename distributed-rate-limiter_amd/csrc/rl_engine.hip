@@ -499,7 +499,7 @@ constexpr uint32_t CTRL_NSEG = 0;              // [0..3] list counts (heavy TB, 
 constexpr uint32_t CTRL_DBG = CTRL_NSEG + 8;   // [0] rounds [1] near/exact iterations [2] max rounds
                                                // [3..6] round ends (full, stop, partial, first window)
                                                // [8..19] timers [20] exact tiles [21] serial steps
-constexpr uint32_t CTRL_DBGN = 96;
+constexpr uint32_t CTRL_DBGN = 88;
 constexpr uint32_t CTRL_HEAD = CTRL_DBG + CTRL_DBGN;  // words zeroed by k_probe
 constexpr uint32_t CTRL_HIST = CTRL_HEAD;             // [4][256]
 constexpr uint32_t CTRL_TILE = CTRL_HIST + 4 * RADIX;  // [4] tile counters

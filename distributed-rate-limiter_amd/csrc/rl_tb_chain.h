@@ -1665,7 +1665,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     // of one-decade / multi-decade windows and their counts, chain resolve
     // cycles of one-decade / multi-decade windows and their counts
     uint64_t cx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t cplan = 0;   // producer 0: plan cycles (dbg[88])
+    uint64_t cplan = 0;   // producer 0: plan cycles (dbg[48])
 #endif
     (void)t0; (void)t1;
     TbLoader L;
@@ -1986,7 +1986,7 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[24 + 4 * role + k], (uint32_t)(cyc[k] >> 4));
         if (role == 1) {
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 2 ? cx[k] >> 4 : cx[k]));
-            atomicAdd(&dbg[88], (uint32_t)(cplan >> 4));
+            atomicAdd(&dbg[48], (uint32_t)(cplan >> 4));
         }
         if (role == 0) {
             for (int k = 4; k < 8; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 6 ? cx[k] >> 4 : cx[k]));

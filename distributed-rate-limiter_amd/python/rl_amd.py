@@ -343,7 +343,7 @@ class Engine:
             return None
         return out.reshape(256, 6)
 
-    def debug_words(self, n=96) -> np.ndarray:
+    def debug_words(self, n=88) -> np.ndarray:
         out = np.zeros(n, np.uint32)
         lib.rl_engine_debug_words(self.h, _ptr(out), n)
         return out
