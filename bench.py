@@ -531,6 +531,8 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "chain_round_tops_x16": int(dbgw[87]) * 16,
                           # stamps build: producer 0's plan cycles (after the exit guess)
                           "producer_plan_x16": int(dbgw[48]) * 16,
+                          # of which in the window-plan calls: count, cycles
+                          "plan_calls": [int(dbgw[49]), int(dbgw[50]) * 16],
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)

@@ -1628,12 +1628,17 @@ __device__ XDEC_FN ChOutcome ch_resolve_x(ChainLds* shp, ChState s, XScale xs, R
     return o;
 }
 
+#ifdef RL_PLAN_INLINE   // A/B: the plan inlined into the producers' round (no call)
+#define PLAN_FN __attribute__((always_inline)) inline
+#else
+#define PLAN_FN XDEC_FN
+#endif
 struct XPlanW {
     int32_t mode;
     int32_t E;
     double vt;        // the calling producer's tile start estimate
 };
-__device__ XDEC_FN XPlanW ch_plan_w(ChainLds* shp, uint32_t first, uint32_t cnt, double v0,
+__device__ PLAN_FN XPlanW ch_plan_w(ChainLds* shp, uint32_t first, uint32_t cnt, double v0,
                                                     uint32_t pw, uint32_t seq) {
     ChainShared& sh = *(ChainShared*)shp;
 #ifdef RL_PLAN_SEQ   // A/B: every producer wave sums the whole window
@@ -1666,6 +1671,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
     // cycles of one-decade / multi-decade windows and their counts
     uint64_t cx[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t cplan = 0;   // producer 0: plan cycles (dbg[48])
+    uint64_t cpcall = 0;  // of which in ch_plan_w calls (dbg[50]), npcall of them (dbg[49])
+    uint32_t npcall = 0;
 #endif
     (void)t0; (void)t1;
     TbLoader L;
@@ -1789,7 +1796,16 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
             double dmax = (double)DEC_HI;
             if (sp.valid) {
                 if (xd) {
+#ifdef RL_STAMPS
+                    uint64_t tq0, tq1;
+                    CH_T(tq0);
+#endif
                     pl = ch_plan_w(shl, sp.first, sp.cnt, sp.v0, pw, ++plan_seq);
+#ifdef RL_STAMPS
+                    CH_T(tq1);
+                    cpcall += tq1 - tq0;
+                    npcall++;
+#endif
                     if (pl.mode == QM_NONE) sp.valid = 0u;
                 } else {
                     pl.mode = QM_DEC;
@@ -1830,7 +1846,16 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
 #pragma unroll
                         for (int t = 0; t < CH_NP; t++) Xe += (uint32_t)t < nt ? sh.tile[s.cbuf][t].S : 0;
                     }
+#ifdef RL_STAMPS
+                    uint64_t tq0, tq1;
+                    CH_T(tq0);
+#endif
                     pl = ch_plan_w(shl, wf, wc, st_value(Xe, s.E, s.mode), pw, ++plan_seq);
+#ifdef RL_STAMPS
+                    CH_T(tq1);
+                    cpcall += tq1 - tq0;
+                    npcall++;
+#endif
                 }
             }
 #ifdef RL_STAMPS
@@ -1987,6 +2012,8 @@ __device__ __attribute__((always_inline)) inline void ch_segment(ChainShared& sh
         if (role == 1) {
             for (int k = 0; k < 4; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 2 ? cx[k] >> 4 : cx[k]));
             atomicAdd(&dbg[48], (uint32_t)(cplan >> 4));
+            atomicAdd(&dbg[49], npcall);
+            atomicAdd(&dbg[50], (uint32_t)(cpcall >> 4));
         }
         if (role == 0) {
             for (int k = 4; k < 8; k++) atomicAdd(&dbg[70 + k], (uint32_t)(k < 6 ? cx[k] >> 4 : cx[k]));
