@@ -283,6 +283,14 @@ def roofline_of(replay_ms, algs, uniq, m, workload):
             "launch_ms": per_launch_ms[dom]}, per_launch_ms
 
 
+def _rel_us(dbgw, k):
+    """debug word k (10-ns realtime ticks, low 32 bits) in us after the replay's first block start
+    (dbg[13] holds its complement); None when unset (product builds)"""
+    if not int(dbgw[k]):
+        return None
+    return ((int(dbgw[k]) - (~int(dbgw[13]) & 0xffffffff)) & 0xffffffff) / 100
+
+
 def hot_chain_us(dbgw):
     """the last batch's longest huge segment (the hot key's chain), start to
     end in microseconds (replay kernel timeline words, 10 ns ticks)"""
@@ -533,6 +541,12 @@ def bench_local(args, workload, world, rank, local_rank, dev, sharded):
                           "producer_plan_x16": int(dbgw[48]) * 16,
                           # of which in the window-plan calls: count, cycles
                           "plan_calls": [int(dbgw[49]), int(dbgw[50]) * 16],
+                          # stamps build: the replay's tail (us from the first block's start): the
+                          # latest block start, the latest end of a heavy phase, the latest light
+                          # claim that got work; the longest heavy segment's replay (us, length)
+                          "replay_tail_us": {"last_block_start": _rel_us(dbgw, 51), "last_heavy_end": _rel_us(dbgw, 53),
+                                             "last_light_claim": _rel_us(dbgw, 54),
+                                             "longest_heavy_segment": [int(dbgw[56]) / 100, int(dbgw[57])]},
                           # stamps build: the hot chain's exact tiles (cycles, passes)
                           "exact_hot_x16": [int(dbgw[7]) * 16, int(dbgw[11])],
                           # batches whose grouping sort ran as k_sort_local alone (predicted plan)

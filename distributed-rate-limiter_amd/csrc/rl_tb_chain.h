@@ -2147,7 +2147,17 @@ __device__ __attribute__((always_inline)) inline void replay_rest(const uint32_t
             for (uint32_t u = u0; u < u1; u++) {
                 if (u < nhx + nheavy) {
                     const SegRec sg = u < nhx ? L.list[3][u] : L.list[0][u - nhx];
+#ifdef RL_STAMPS
+                    const uint64_t th0 = __builtin_amdgcn_s_memrealtime();
+#endif
                     wave_segment(&tb[sk[sg.j0]], sg.j0, sg.j0 + sg.len, cfgs, profile, a, pre, eflags, iters);
+#ifdef RL_STAMPS
+                    // the longest heavy segment's replay (dbg[56], ticks) and its length (dbg[57])
+                    if ((threadIdx.x & 63) == 0 && dbg) {
+                        const uint32_t dt = (uint32_t)(__builtin_amdgcn_s_memrealtime() - th0);
+                        if (atomicMax(&dbg[56], dt) < dt) dbg[57] = sg.len;
+                    }
+#endif
                 } else {
                     const SegRec sg = L.list[2][u - nhx - nheavy];
                     wave_win_segment(&win[sk[sg.j0] - win_base], spill, sg.j0, sg.j0 + sg.len, cfgs, profile, a,
@@ -2158,12 +2168,20 @@ __device__ __attribute__((always_inline)) inline void replay_rest(const uint32_t
     }
     __syncthreads();
     const uint64_t t_light = __builtin_amdgcn_s_memrealtime();
+#ifdef RL_STAMPS
+    // the latest end of a block's heavy phase (dbg[53])
+    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[53], (uint32_t)t_light);
+#endif
     for (;;) {
         if (threadIdx.x == 0) s_u = atomicAdd(&qctr[1], (uint32_t)blockDim.x);
         __syncthreads();
         const uint32_t u0 = s_u;
         __syncthreads();
         if (u0 >= nlight) break;
+#ifdef RL_STAMPS
+        // the latest light claim that got work (dbg[54])
+        if (threadIdx.x == 0 && dbg) atomicMax(&dbg[54], (uint32_t)__builtin_amdgcn_s_memrealtime());
+#endif
         const uint32_t u = u0 + threadIdx.x;
         if (u < nlight) {
             const SegRec sg = L.list[1][u];
@@ -2221,6 +2239,11 @@ __global__ __launch_bounds__(CH_BLOCK) void k_tb_chain(const uint32_t* __restric
     // timeline (10 ns ticks, low 32 bits): dbg[13] = ~first block start,
     // dbg[14] = last block end, dbg[16/17] = longest segment start / end
     if (threadIdx.x == 0 && dbg) atomicMax(&dbg[13], ~(uint32_t)__builtin_amdgcn_s_memrealtime());
+#ifdef RL_STAMPS
+    // the replay's tail: the latest block start (dbg[51]; all four are 10-ns
+    // realtime ticks, low 32 bits)
+    if (threadIdx.x == 0 && dbg) atomicMax(&dbg[51], (uint32_t)__builtin_amdgcn_s_memrealtime());
+#endif
     for (;;) {
         // claim the longest unclaimed huge segment (their list is short:
         // batch / 4096 at most), so the hottest key starts with the first
