@@ -195,6 +195,20 @@ def test_long_windows(rl, profile, alg, wi):
     run_both(rl, profile, configs, split(tr, [3000, 27_000, 90_000]), tb=1 << 16, win=1 << 16)
 
 
+@pytest.mark.parametrize("alg,profile,wi", [(1, 0, 0), (2, 1, 1), (3, 0, 2), (0, 1, 0)])
+def test_long_windows_many_keys(rl, alg, profile, wi, monkeypatch):
+    """The long-window configurations over many light keys and no hot key:
+    k_small (batches up to 4096), the full launch sequence, then batches of
+    2^19 and more, which after the first take the light replay kernel
+    (k_replay_light)."""
+    monkeypatch.setenv("RL_SMALL_MAX", "4096")
+    configs, tr = long_window_trace(1300 + 10 * wi + alg + 5 * profile, alg, 1_300_000, wi=wi,
+                                    n_light=50_000, hot_share=0.0)
+    eng, _ = run_both(rl, profile, configs, split(tr, [3000, 4096, 90_000, 600_000, 602_904]),
+                      tb=1 << 17, win=1 << 17)
+    assert eng.stats().light_batches >= 1
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_random_configs_many_keys(rl, seed, monkeypatch):
     """The same random configurations over many keys: batches below the

@@ -131,7 +131,11 @@ def long_window_trace(seed, alg, m, wi=0, n_light=20_000, hot_share=0.6):
     f = np.repeat(10 ** rng.uniform(-6, -0.5, ph), 3000)[:m]
     scale = np.repeat(10 ** rng.uniform(-2, 1, ph), 3000)[:m]
     n = np.maximum(1, np.rint(lim * f)).astype(np.int64) * rng.choice([1, 1, 1, 2], m)
-    gaps = np.rint(rng.exponential(1.0, m) * np.minimum(period * n * scale * hot_share / 3, 1e12))
+    # a key with share s of the traffic sees one request per gap / s: its
+    # consumption keeps pace with its refill at scale ~1 (no hot keys: every
+    # key a light one, s = 1 / n_light)
+    share = hot_share / 3 if hot_share > 0 else 1.0 / n_light
+    gaps = np.rint(rng.exponential(1.0, m) * np.minimum(period * n * scale * share, 1e12))
     gaps[rng.random(m) < 0.05] = 0
     jumps = rng.choice([0, 3600 * NS, DAY, 5 * DAY, 40 * DAY, 400 * DAY], ph, p=[0.3, 0.2, 0.2, 0.15, 0.1, 0.05])
     jumps = (jumps * rng.random(ph)).astype(np.int64)
