@@ -347,7 +347,7 @@ def _free_port():
     return p
 
 
-def _routed_rank(rank, world, port, backend, batches_of, q, exchange=None, cap=None):
+def _routed_rank(rank, world, port, backend, batches_of, q, exchange=None, cap=None, configs=None, profile=0):
     """one rank of the native routed path on cuda:0: Router kernels, the HIP
     engine as owner (rl_decide_routed_device), equal-split all-to-alls over
     `backend` (nccl: RCCL; gloo: through host memory, for two ranks sharing
@@ -371,9 +371,10 @@ def _routed_rank(rank, world, port, backend, batches_of, q, exchange=None, cap=N
         mine = all_batches[rank]
         mb = max(b[0].size for b in mine)
         router = rl_amd.Router(0, world, mb, cap or mb)
-        eng = rl_amd.Engine(profile=0, tb_capacity=1 << 20, win_capacity=1 << 20,
+        eng = rl_amd.Engine(profile=profile, tb_capacity=1 << 20, win_capacity=1 << 20,
                             max_batch=world * router.capacity)
-        for a, L, W in CONFIGS:
+        configs = configs or CONFIGS
+        for a, L, W in configs:
             eng.register(a, L, W)
         pg_res = dist.new_group(backend=backend)
         pipe = shard.RoutedPipeline(router, eng.decide_routed, world, mb, "cuda:0", pg_req=None, pg_res=pg_res,
@@ -388,7 +389,8 @@ def _routed_rank(rank, world, port, backend, batches_of, q, exchange=None, cap=N
         info["router_status"] = router.sync(None)
         info["collectives"] = pipe.collectives
         info["exchange"] = pipe.exchange
-        exp = route_ops.shared_limiter_expectations(all_batches, rank, CONFIGS, cap=router.capacity)
+        exp = route_ops.shared_limiter_expectations(all_batches, rank, configs, profile=profile,
+                                                    cap=router.capacity)
         ok = True
         for b, (ob, eb) in enumerate(zip(outs, exp)):
             for f, (o, e) in enumerate(zip(ob, eb)):
@@ -497,3 +499,38 @@ def test_routed_path_one_rank_unsorted_batches():
 
 def test_routed_path_two_ranks_unsorted_batches():
     _check(_spawn(2, "gloo", skewed_batches), 2, 3, True)
+
+
+LONG_SEED = 1500
+
+
+def long_window_batches(rank, nbatch=3, world=2):
+    """one long-window trace (tracegen.long_window_trace: 1-365 d windows,
+    L = 1, three hot keys, phase jumps of up to 400 days) dealt to the ranks
+    request by request, so the ranks' clocks interleave; each rank's share in
+    nbatch steps"""
+    import tracegen
+    _, (k, ts, n, cfg, _) = tracegen.long_window_trace(LONG_SEED, 0, 180_000, wi=0)
+    k, ts, n, cfg = (x[rank::world] for x in (k, ts, n, cfg))
+    m = k.size // nbatch
+    return [(k[b * m:(b + 1) * m], ts[b * m:(b + 1) * m], n[b * m:(b + 1) * m], cfg[b * m:(b + 1) * m])
+            for b in range(nbatch)]
+
+
+def _long_configs():
+    import tracegen
+    return tracegen.long_window_trace(LONG_SEED, 0, 10, wi=0)[0]
+
+
+@pytest.mark.parametrize("profile", [0, 1])
+def test_routed_path_one_rank_long_windows(profile):
+    """world size 1 over RCCL (exchange forced on) with reference-legal long
+    windows (config.go:41-46): the store clock carries years of phase jumps
+    through the merge and the engine's explicit-clock records"""
+    import functools
+    _check(_spawn(1, "nccl", functools.partial(long_window_batches, world=1), exchange=True,
+                  configs=_long_configs(), profile=profile), 1, 3, True)
+
+
+def test_routed_path_two_ranks_long_windows():
+    _check(_spawn(2, "gloo", long_window_batches, configs=_long_configs(), profile=1), 2, 3, True)
