@@ -659,6 +659,36 @@ def test_table_gc_keeps_decisions(rl, profile):
         assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
 
 
+@pytest.mark.parametrize("profile", [0, 1])
+def test_table_gc_long_windows(rl, profile):
+    """GC between batches of the long-window trace (windows of 1-365 days,
+    TTLs that long, phase jumps of up to 400 days: keys expire between and
+    within batches), with a grow and a shrink on the way: decisions stay the
+    oracle's, and GC keeps exactly the live keys."""
+    configs, tr = long_window_trace(1600 + profile, 0, 120_000, wi=profile, n_light=8_000)
+    eng = make_engine(rl, profile, tb=1 << 15, win=1 << 15, max_batch=1 << 15)
+    sim = oracle.OracleSim(profile)
+    for a, L, W in configs:
+        assert eng.register(a, L, W) == sim.add_config(a, L, W)
+    parts = split(tr, [20_000] * 6)
+    caps = [(0, 0), (1 << 16, 1 << 16), (0, 0), (1 << 14, 1 << 14), (0, 0)]
+    collected = 0
+    for i, (key, ts, n, cfg, sms) in enumerate(parts):
+        if i:
+            now_ms = int(ts[0]) // 1_000_000
+            before = eng.table_info(now_ms)
+            _, after = eng.table_gc(now_ms, *caps[i - 1])
+            assert after.tb_live == before.tb_live and after.win_live == before.win_live
+            assert after.tb_used == after.tb_live <= before.tb_used
+            collected += (before.tb_used - after.tb_used) + (before.win_used - after.win_used)
+            if caps[i - 1][0]:
+                assert after.tb_capacity == caps[i - 1][0] and after.win_capacity == caps[i - 1][1]
+        res = eng.decide(key, ts, n, cfg, sms)
+        assert_same(res, sim.decide(key, ts, n, cfg, sms), configs, cfg, what=f"batch {i}")
+    assert collected > 0          # the phase jumps expired keys that GC then dropped
+    eng.close()
+
+
 def test_table_gc_frees_a_full_table(rl):
     """A table that is full of expired keys accepts new keys after GC; a GC
     whose live keys do not fit the requested size fails and keeps the tables."""
