@@ -117,6 +117,14 @@ def test_routed_pipeline_matches_single_shared_limiter():
     assert _run_ranks(2) == {0: (True, False), 1: (True, False)}
 
 
+@pytest.mark.parametrize("world", [3, 4])
+def test_routed_pipeline_more_ranks(world):
+    """the same at world size 3 and 4 (the driver's 8-GPU run has 2, 4 and 8
+    ranks; more CPU ranks than this only slow the suite): per-peer buckets,
+    the merge of 3-4 sources per owner and the one collective order"""
+    assert _run_ranks(world) == {r: (True, False) for r in range(world)}
+
+
 def test_routed_pipeline_bucket_overflow_drops_requests():
     """buckets smaller than a rank's requests for one owner: the requests past
     the capacity are dropped at the sender (RL_DROPPED, never applied) and
