@@ -618,9 +618,11 @@ struct rl_engine {
     int next_set = 0, last_set = 0;   // set of the next / the last enqueued batch
     size_t zero_bytes = 0;
     int coop_grid = 128;        // k_tb_chain blocks launched (one per CU fits its LDS) ...
-    int coop_base = 96;         // ... of which those past 96 of 256 CUs exit at once unless the batch
+    int coop_base = 112;        // ... of which those past 112 of 256 CUs exit at once unless the batch
                                 // has at least m / coop_light_div light segments: the other CUs run
-                                // the neighbouring batches' grouping and finish (profiles/r3al_ab_replay_grid.txt)
+                                // the neighbouring batches' grouping and finish (profiles/r3al_ab_replay_grid.txt;
+                                // 96 -> 112 with the iterative-ILP build: configs[1] +1.1-1.5 %,
+                                // profiles/r6zm_ab_coop_base.txt)
     uint32_t coop_light_div = 4;
     int probe_grid = 1024;      // k_probe blocks at most
     int perm_grid = 1024;       // k_permute / k_unpermute blocks at most
